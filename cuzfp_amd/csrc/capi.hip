@@ -1,0 +1,376 @@
+// cuzfp_amd/csrc/capi.hip -- the C-ABI of include/cuzfp_hip.h: argument
+// checking, kernel dispatch and the pinned host-memory pipeline.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "launch.hpp"
+
+namespace cuzfp {
+
+thread_local int t_last_hip = hipSuccess;
+
+static int make_problem(int type, unsigned nx, unsigned ny, unsigned nz, long long sx,
+                        long long sy, long long sz, unsigned maxbits, Problem* pr) {
+  if (type < CUZFP_TYPE_INT32 || type > CUZFP_TYPE_DOUBLE) return CUZFP_ERROR_UNSUPPORTED_TYPE;
+  if (!nx || (nz && !ny)) return CUZFP_ERROR_INVALID_ARGUMENT;
+  const unsigned dims = nz ? 3 : ny ? 2 : 1;
+  const unsigned ebits = type == CUZFP_TYPE_FLOAT ? 9 : type == CUZFP_TYPE_DOUBLE ? 12 : 1;
+  // LDS image of one wave's segment must fit a workgroup's 64 KiB
+  if (maxbits < ebits || maxbits > 8000) return CUZFP_ERROR_INVALID_ARGUMENT;
+  Geometry& g = pr->g;
+  g.nx = nx;
+  g.ny = dims > 1 ? ny : 1;
+  g.nz = dims > 2 ? nz : 1;
+  g.bx = (g.nx + 3) / 4;
+  g.by = (g.ny + 3) / 4;
+  const uint64_t nb = (uint64_t)g.bx * g.by * ((g.nz + 3) / 4);
+  if (nb >= (1ull << 32) - kLanes) return CUZFP_ERROR_INVALID_ARGUMENT;
+  g.nblocks = (uint32_t)nb;
+  g.maxbits = maxbits;
+  g.wave0 = 0;
+  g.vec_io = 0;
+  g.sx = sx ? sx : 1;
+  g.sy = sy ? sy : (long long)g.nx;
+  g.sz = sz ? sz : (long long)g.nx * g.ny;
+  pr->type = type;
+  pr->dims = dims;
+  pr->fast_ok = (type == CUZFP_TYPE_FLOAT || type == CUZFP_TYPE_DOUBLE) && g.sx == 1 &&
+                g.sy == (long long)g.nx && g.sz == (long long)g.nx * g.ny && g.nx % 4 == 0 &&
+                (dims < 2 || g.ny % 4 == 0) && (dims < 3 || g.nz % 4 == 0);
+  return CUZFP_SUCCESS;
+}
+
+static int launch_encode(const Problem& p, const void* data, uint64_t* stream, uint32_t wave0,
+                         uint32_t nwaves, hipStream_t st) {
+  if (!nwaves) return CUZFP_SUCCESS;
+  const bool fast = p.fast_ok && ((uintptr_t)data & 15) == 0;
+  switch (p.type) {
+    case CUZFP_TYPE_INT32: return launch_encode_type<int32_t>(p, data, false, stream, wave0, nwaves, st);
+    case CUZFP_TYPE_INT64: return launch_encode_type<int64_t>(p, data, false, stream, wave0, nwaves, st);
+    case CUZFP_TYPE_FLOAT: return launch_encode_type<float>(p, data, fast, stream, wave0, nwaves, st);
+    default: return launch_encode_type<double>(p, data, fast, stream, wave0, nwaves, st);
+  }
+}
+
+static int launch_decode(const Problem& p, const uint64_t* stream, void* data, uint32_t wave0,
+                         uint32_t nwaves, hipStream_t st) {
+  if (!nwaves) return CUZFP_SUCCESS;
+  const bool fast = p.fast_ok && ((uintptr_t)data & 15) == 0;
+  switch (p.type) {
+    case CUZFP_TYPE_INT32: return launch_decode_type<int32_t>(p, stream, false, data, wave0, nwaves, st);
+    case CUZFP_TYPE_INT64: return launch_decode_type<int64_t>(p, stream, false, data, wave0, nwaves, st);
+    case CUZFP_TYPE_FLOAT: return launch_decode_type<float>(p, stream, fast, data, wave0, nwaves, st);
+    default: return launch_decode_type<double>(p, stream, fast, data, wave0, nwaves, st);
+  }
+}
+
+static size_t stream_bytes_of(const Geometry& g) {
+  return (((size_t)g.nblocks * g.maxbits + 63) / 64) * 8;
+}
+
+static uint32_t waves_of(const Geometry& g) { return (g.nblocks + kLanes - 1) / kLanes; }
+
+
+// ---------------------------------------------------------------------------
+// Host-memory pipeline (cuzfp_hip_compress_host / cuzfp_hip_decompress_host).
+//
+// The array is cut into chunks of whole block slabs along its slowest axis
+// (4 z-planes in 3D, 4 rows in 2D, 4 values in 1D), ~kChunkBytes of scalars
+// each.  Chunk i runs on stream i % S:
+//   encode: H2D slabs -> encode the waves whose blocks are now all resident
+//           -> D2H their stream words
+//   decode: H2D the stream words of a wave range -> decode -> D2H the slabs
+//           whose blocks are now all decoded
+// Waves straddle slab boundaries, so each kernel / D2H also waits on the
+// previous S-1 chunks' events (chunks further back ran on the same streams).
+// Pinned (hipHostMalloc / registered) user buffers are DMA'd in place;
+// pageable ones go through a ring of pinned staging buffers.
+
+constexpr size_t kChunkBytes = 32u << 20;
+
+static bool is_pinned_host(const void* ptr) {
+  hipPointerAttribute_t a;
+  const hipError_t e = hipPointerGetAttributes(&a, ptr);
+  (void)hipGetLastError();
+  return e == hipSuccess && a.type == hipMemoryTypeHost;
+}
+
+namespace {
+struct Chunk {
+  size_t d0, d1;    // data byte range
+  size_t s0, s1;    // stream byte range
+  uint32_t w0, w1;  // wave range for the kernel
+};
+
+struct PipelineRes {
+  std::vector<hipStream_t> st;
+  std::vector<hipEvent_t> ev_in, ev_kernel, ev_done;
+  std::vector<void*> pin_in, pin_out;
+  void* d_data = nullptr;
+  void* d_stream = nullptr;
+  ~PipelineRes() {
+    for (auto s : st) (void)hipStreamDestroy(s);
+    for (auto e : ev_in) (void)hipEventDestroy(e);
+    for (auto e : ev_kernel) (void)hipEventDestroy(e);
+    for (auto e : ev_done) (void)hipEventDestroy(e);
+    for (auto b : pin_in) (void)hipHostFree(b);
+    for (auto b : pin_out) (void)hipHostFree(b);
+    if (d_data) (void)hipFree(d_data);
+    if (d_stream) (void)hipFree(d_stream);
+  }
+};
+}  // namespace
+
+#define CUZFP_HIP_TRY(x)            \
+  do {                              \
+    const hipError_t e_ = (x);      \
+    if (e_ != hipSuccess) {         \
+      t_last_hip = e_;              \
+      return CUZFP_ERROR_HIP;       \
+    }                               \
+  } while (0)
+
+static int host_pipeline(const Problem& p, bool encode, void* h_data, void* h_stream,
+                         int nstreams) {
+  const Geometry& g = p.g;
+  const size_t es = (p.type == CUZFP_TYPE_FLOAT || p.type == CUZFP_TYPE_INT32) ? 4 : 8;
+  // slabs along the slowest axis
+  const size_t slab_vals = p.dims == 3 ? 4ull * g.nx * g.ny : p.dims == 2 ? 4ull * g.nx : 4ull;
+  const size_t slab_blocks = p.dims == 3 ? (size_t)g.bx * g.by : p.dims == 2 ? g.bx : 1;
+  const size_t total_vals = (size_t)g.nx * g.ny * g.nz;
+  const size_t nslabs = ((size_t)(p.dims == 3 ? g.nz : p.dims == 2 ? g.ny : g.nx) + 3) / 4;
+  const uint32_t nwaves = waves_of(g);
+  const size_t data_bytes = total_vals * es;
+  const size_t sbytes = stream_bytes_of(g);
+  const size_t wave_bytes = (size_t)g.maxbits * 8;  // stream bytes per full wave
+  const size_t per = std::max<size_t>(1, kChunkBytes / (slab_vals * es));
+
+  std::vector<Chunk> chunks;
+  uint32_t w_prev = 0;
+  size_t d_prev = 0;
+  for (size_t s = 0; s < nslabs; s += per) {
+    const size_t e = std::min(nslabs, s + per);
+    const bool last = e == nslabs;
+    Chunk c;
+    if (encode) {
+      c.d0 = std::min(data_bytes, s * slab_vals * es);
+      c.d1 = last ? data_bytes : e * slab_vals * es;
+      c.w0 = w_prev;
+      c.w1 = last ? nwaves : (uint32_t)(e * slab_blocks / kLanes);
+      w_prev = c.w1;
+    } else {
+      c.w0 = w_prev;
+      c.w1 = last ? nwaves : (uint32_t)(e * slab_blocks / kLanes);
+      w_prev = c.w1;
+      const size_t done_slabs = last ? nslabs : (size_t)c.w1 * kLanes / slab_blocks;
+      c.d0 = d_prev;
+      c.d1 = std::min(data_bytes, done_slabs * slab_vals * es);
+      d_prev = c.d1;
+    }
+    c.s0 = std::min(sbytes, (size_t)c.w0 * wave_bytes);
+    c.s1 = last ? sbytes : std::min(sbytes, (size_t)c.w1 * wave_bytes);
+    chunks.push_back(c);
+  }
+
+  const int S = std::max(1, std::min(nstreams, 8));
+  const bool data_pinned = is_pinned_host(h_data);
+  const bool stream_pinned = is_pinned_host(h_stream);
+  PipelineRes r;
+  CUZFP_HIP_TRY(hipMalloc(&r.d_data, std::max<size_t>(data_bytes, 16)));
+  CUZFP_HIP_TRY(hipMalloc(&r.d_stream, std::max<size_t>(sbytes, 16)));
+  size_t max_in = 0, max_out = 0;
+  for (const Chunk& c : chunks) {
+    max_in = std::max(max_in, encode ? c.d1 - c.d0 : c.s1 - c.s0);
+    max_out = std::max(max_out, encode ? c.s1 - c.s0 : c.d1 - c.d0);
+  }
+  const bool in_pinned = encode ? data_pinned : stream_pinned;
+  const bool out_pinned = encode ? stream_pinned : data_pinned;
+  r.st.resize(S);
+  r.ev_in.resize(S);
+  r.ev_kernel.resize(S);
+  r.ev_done.resize(S);
+  for (int i = 0; i < S; i++) {
+    CUZFP_HIP_TRY(hipStreamCreateWithFlags(&r.st[i], hipStreamNonBlocking));
+    CUZFP_HIP_TRY(hipEventCreateWithFlags(&r.ev_in[i], hipEventDisableTiming));
+    CUZFP_HIP_TRY(hipEventCreateWithFlags(&r.ev_kernel[i], hipEventDisableTiming));
+    CUZFP_HIP_TRY(hipEventCreateWithFlags(&r.ev_done[i], hipEventDisableTiming));
+    void* b = nullptr;
+    if (!in_pinned) {
+      CUZFP_HIP_TRY(hipHostMalloc(&b, std::max<size_t>(max_in, 16), hipHostMallocDefault));
+      r.pin_in.push_back(b);
+    }
+    if (!out_pinned) {
+      CUZFP_HIP_TRY(hipHostMalloc(&b, std::max<size_t>(max_out, 16), hipHostMallocDefault));
+      r.pin_out.push_back(b);
+    }
+  }
+  char* hd = (char*)h_data;
+  char* hs = (char*)h_stream;
+  char* dd = (char*)r.d_data;
+  char* ds = (char*)r.d_stream;
+  auto out_range = [&](const Chunk& c, size_t* o0, size_t* o1) {
+    *o0 = encode ? c.s0 : c.d0;
+    *o1 = encode ? c.s1 : c.d1;
+  };
+  const size_t n = chunks.size();
+  for (size_t i = 0; i < n + S; i++) {
+    // retire chunk i - S: its slot's buffers become free
+    if (i >= (size_t)S) {
+      const size_t j = i - S;
+      const int sj = (int)(j % S);
+      CUZFP_HIP_TRY(hipEventSynchronize(r.ev_done[sj]));
+      if (!out_pinned) {
+        size_t o0, o1;
+        out_range(chunks[j], &o0, &o1);
+        if (o1 > o0) std::memcpy((encode ? hs : hd) + o0, r.pin_out[sj], o1 - o0);
+      }
+    }
+    if (i >= n) continue;
+    const Chunk& c = chunks[i];
+    const int s = (int)(i % S);
+    hipStream_t st = r.st[s];
+    // input copy
+    const size_t i0 = encode ? c.d0 : c.s0, i1 = encode ? c.d1 : c.s1;
+    char* src = (encode ? hd : hs) + i0;
+    char* dst = (encode ? dd : ds) + i0;
+    if (i1 > i0) {
+      if (!in_pinned) {
+        std::memcpy(r.pin_in[s], src, i1 - i0);
+        src = (char*)r.pin_in[s];
+      }
+      CUZFP_HIP_TRY(hipMemcpyAsync(dst, src, i1 - i0, hipMemcpyHostToDevice, st));
+    }
+    CUZFP_HIP_TRY(hipEventRecord(r.ev_in[s], st));
+    // encode kernel over waves [w0, w1): needs the neighbouring chunks' input
+    if (encode)
+      for (size_t k = (i >= (size_t)S - 1 ? i - S + 1 : 0); k < i; k++)
+      CUZFP_HIP_TRY(hipStreamWaitEvent(st, r.ev_in[k % S], 0));
+    int rc = encode ? launch_encode(p, dd, (uint64_t*)ds, c.w0, c.w1 - c.w0, st)
+                    : launch_decode(p, (const uint64_t*)ds, dd, c.w0, c.w1 - c.w0, st);
+    if (rc) return rc;
+    CUZFP_HIP_TRY(hipEventRecord(r.ev_kernel[s], st));
+    // output copy: decoded slabs may contain blocks of earlier chunks' kernels
+    if (!encode)
+      for (size_t k = (i >= (size_t)S - 1 ? i - S + 1 : 0); k < i; k++)
+        CUZFP_HIP_TRY(hipStreamWaitEvent(st, r.ev_kernel[k % S], 0));
+    size_t o0, o1;
+    out_range(c, &o0, &o1);
+    if (o1 > o0) {
+      char* osrc = (encode ? ds : dd) + o0;
+      char* odst = out_pinned ? (encode ? hs : hd) + o0 : (char*)r.pin_out[s];
+      CUZFP_HIP_TRY(hipMemcpyAsync(odst, osrc, o1 - o0, hipMemcpyDeviceToHost, st));
+    }
+    CUZFP_HIP_TRY(hipEventRecord(r.ev_done[s], st));
+  }
+  return CUZFP_SUCCESS;
+}
+
+}  // namespace cuzfp
+
+
+// ---------------------------------------------------------------------------
+// C-ABI
+
+using namespace cuzfp;
+
+extern "C" {
+
+int cuzfp_hip_abi_version(void) { return CUZFP_HIP_ABI_VERSION; }
+
+const char* cuzfp_hip_status_string(int status) {
+  switch (status) {
+    case CUZFP_SUCCESS: return "success";
+    case CUZFP_ERROR_INVALID_ARGUMENT: return "invalid argument";
+    case CUZFP_ERROR_UNSUPPORTED_TYPE: return "unsupported scalar type";
+    case CUZFP_ERROR_BUFFER_TOO_SMALL: return "stream buffer too small";
+    case CUZFP_ERROR_HIP: return "HIP runtime error";
+  }
+  return "unknown status";
+}
+
+int cuzfp_hip_last_hip_error(void) { return t_last_hip; }
+
+unsigned cuzfp_hip_rate_to_maxbits(double rate, int type, unsigned dims, int wra) {
+  if (dims < 1 || dims > 3 || !(rate >= 0)) return 0;
+  const unsigned n = 1u << (2 * dims);
+  unsigned bits = (unsigned)floor(n * rate + 0.5);
+  if (type == CUZFP_TYPE_FLOAT) bits = std::max(bits, 1u + 8u);
+  if (type == CUZFP_TYPE_DOUBLE) bits = std::max(bits, 1u + 11u);
+  if (wra) bits = (bits + 63) & ~63u;
+  return bits;
+}
+
+size_t cuzfp_hip_stream_bytes(int type, unsigned nx, unsigned ny, unsigned nz, unsigned maxbits) {
+  Problem p;
+  if (make_problem(type, nx, ny, nz, 0, 0, 0, maxbits, &p) != CUZFP_SUCCESS) return 0;
+  return stream_bytes_of(p.g);
+}
+
+size_t cuzfp_hip_maximum_size(int type, unsigned nx, unsigned ny, unsigned nz, unsigned maxbits) {
+  // zfp_structs.h:237-266 with the reference's header allowance of 148 bits
+  Problem p;
+  if (make_problem(type, nx, ny, nz, 0, 0, 0, maxbits, &p) != CUZFP_SUCCESS) return 0;
+  const unsigned values = 1u << (2 * p.dims);
+  const unsigned prec = (type == CUZFP_TYPE_FLOAT || type == CUZFP_TYPE_INT32) ? 32 : 64;
+  unsigned mb = 1 + (type == CUZFP_TYPE_FLOAT ? 8 : type == CUZFP_TYPE_DOUBLE ? 11 : 0);
+  mb += values - 1 + values * prec;
+  mb = std::min(mb, maxbits);
+  return ((148 + (size_t)p.g.nblocks * mb + 63) & ~(size_t)63) / 8;
+}
+
+int cuzfp_hip_encode(const void* d_data, int type, unsigned nx, unsigned ny, unsigned nz,
+                     long long sx, long long sy, long long sz, unsigned maxbits,
+                     uint64_t* d_stream, size_t stream_capacity, size_t* out_bytes,
+                     hipStream_t stream) {
+  Problem p;
+  int rc = make_problem(type, nx, ny, nz, sx, sy, sz, maxbits, &p);
+  if (rc) return rc;
+  if (!d_data || !d_stream) return CUZFP_ERROR_INVALID_ARGUMENT;
+  const size_t need = stream_bytes_of(p.g);
+  if (stream_capacity < need) return CUZFP_ERROR_BUFFER_TOO_SMALL;
+  rc = launch_encode(p, d_data, d_stream, 0, waves_of(p.g), stream);
+  if (rc == CUZFP_SUCCESS && out_bytes) *out_bytes = need;
+  return rc;
+}
+
+int cuzfp_hip_decode(const uint64_t* d_stream, size_t stream_bytes, int type, unsigned nx,
+                     unsigned ny, unsigned nz, long long sx, long long sy, long long sz,
+                     unsigned maxbits, void* d_data, hipStream_t stream) {
+  Problem p;
+  int rc = make_problem(type, nx, ny, nz, sx, sy, sz, maxbits, &p);
+  if (rc) return rc;
+  if (!d_data || !d_stream) return CUZFP_ERROR_INVALID_ARGUMENT;
+  if (stream_bytes < stream_bytes_of(p.g)) return CUZFP_ERROR_BUFFER_TOO_SMALL;
+  return launch_decode(p, d_stream, d_data, 0, waves_of(p.g), stream);
+}
+
+int cuzfp_hip_compress_host(const void* h_data, int type, unsigned nx, unsigned ny,
+                            unsigned nz, unsigned maxbits, void* h_stream,
+                            size_t stream_capacity, size_t* out_bytes, int nstreams) {
+  Problem p;
+  int rc = make_problem(type, nx, ny, nz, 0, 0, 0, maxbits, &p);
+  if (rc) return rc;
+  if (!h_data || !h_stream) return CUZFP_ERROR_INVALID_ARGUMENT;
+  const size_t need = stream_bytes_of(p.g);
+  if (stream_capacity < need) return CUZFP_ERROR_BUFFER_TOO_SMALL;
+  rc = host_pipeline(p, true, (void*)h_data, h_stream, nstreams);
+  if (!rc && out_bytes) *out_bytes = need;
+  return rc;
+}
+
+int cuzfp_hip_decompress_host(const void* h_stream, size_t stream_bytes, int type,
+                              unsigned nx, unsigned ny, unsigned nz, unsigned maxbits,
+                              void* h_data, int nstreams) {
+  Problem p;
+  int rc = make_problem(type, nx, ny, nz, 0, 0, 0, maxbits, &p);
+  if (rc) return rc;
+  if (!h_data || !h_stream) return CUZFP_ERROR_INVALID_ARGUMENT;
+  if (stream_bytes < stream_bytes_of(p.g)) return CUZFP_ERROR_BUFFER_TOO_SMALL;
+  return host_pipeline(p, false, h_data, (void*)h_stream, nstreams);
+}
+
+}  // extern "C"

@@ -1,0 +1,350 @@
+// cuzfp_amd/csrc/kernels.hpp -- MI355X (gfx950) zfp fixed-rate kernels.
+//
+// One zfp block per lane, 64 blocks (one wave) per workgroup:
+//
+//   encode: coalesced 16-byte HBM gathers of the 4^d block  ->  per-lane block
+//           coder (zfp_block.hpp: exponent, quantize, lifting, negabinary,
+//           bit-plane transpose, embedded plane coder)  ->  the lane's bits land
+//           in an LDS image of the wave's contiguous stream segment
+//           (64 * maxbits bits = maxbits words)  ->  one coalesced copy-out.
+//   decode: coalesced copy-in of the wave's stream segment to LDS  ->  per-lane
+//           128-bit window reader + block decoder  ->  16-byte stores.
+//
+// Replaces the reference's six CUDA kernels (src/cuZFP/encode{1,2,3}.cuh,
+// decode{1,2,3}.cuh), which use one 64-thread CTA per 3D block with serial
+// tid-0 packing (encode3.cuh:336-362, decode3.cuh:111-144) and 64-bit global
+// atomics to share stream words in 1D/2D (shared.h:394-424).  Here a wave's
+// stream segment is word aligned (64 * maxbits is a multiple of 64), so
+// workgroups never share a stream word and no global atomics are needed.
+//
+// Instantiated per scalar type in inst_{f32,f64,i32,i64}.hip (parallel build).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "zfp_block.hpp"
+#include "launch.hpp"
+
+namespace cuzfp {
+
+// ---------------------------------------------------------------------------
+// LDS bit writers / reader (one lane, one block)
+
+// maxbits % 64 == 0: the lane owns whole words [lane*W, lane*W + W).
+struct LdsWordWriter {
+  uint64_t* p;
+  uint32_t words, w, cnt;
+  uint64_t acc;
+  __device__ __forceinline__ void put(uint64_t v, unsigned n) {
+    acc |= v << cnt;
+    if (cnt + n >= 64) {
+      p[w++] = acc;
+      acc = cnt ? v >> (64 - cnt) : 0;
+      cnt = cnt + n - 64;
+    } else {
+      cnt += n;
+    }
+  }
+  __device__ __forceinline__ void finish() {
+    if (cnt) p[w++] = acc;
+    while (w < words) p[w++] = 0;
+  }
+};
+
+// general maxbits: the lane's bits start at lane*maxbits; full 64-bit chunks
+// are OR-ed into the (zeroed) LDS image with ds_or_b64, since the first and
+// last words of a lane's range are shared with its neighbours.
+struct LdsBitWriter {
+  uint64_t* lds;
+  uint32_t start, cnt;
+  uint64_t acc;
+  __device__ __forceinline__ void emit(uint64_t v) {
+    const uint32_t w = start >> 6, sh = start & 63;
+    atomicOr((unsigned long long*)&lds[w], (unsigned long long)(v << sh));
+    if (sh) atomicOr((unsigned long long*)&lds[w + 1], (unsigned long long)(v >> (64 - sh)));
+    start += 64;
+  }
+  __device__ __forceinline__ void put(uint64_t v, unsigned n) {
+    acc |= v << cnt;
+    if (cnt + n >= 64) {
+      emit(acc);
+      acc = cnt ? v >> (64 - cnt) : 0;
+      cnt = cnt + n - 64;
+    } else {
+      cnt += n;
+    }
+  }
+  __device__ __forceinline__ void finish() {
+    if (cnt) emit(acc);
+  }
+};
+
+// 128-bit window over the wave's LDS stream image.
+struct LdsReader {
+  const uint64_t* lds;
+  uint64_t w0, w1;
+  uint32_t s, next;
+  __device__ __forceinline__ void init(uint32_t bitpos) {
+    const uint32_t wi = bitpos >> 6;
+    s = bitpos & 63;
+    w0 = lds[wi];
+    w1 = lds[wi + 1];
+    next = wi + 2;
+  }
+  __device__ __forceinline__ uint64_t peek() const { return s ? (w0 >> s) | (w1 << (64 - s)) : w0; }
+  __device__ __forceinline__ void skip(unsigned n) {
+    s += n;
+    if (s >= 64) {
+      s -= 64;
+      w0 = w1;
+      w1 = lds[next++];
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Gather / scatter of one block.  FAST: contiguous layout, every extent a
+// multiple of 4 and a 16-byte aligned base, so each row of 4 values is one
+// 16-byte access and consecutive lanes (consecutive x-blocks) read consecutive
+// 16-byte segments: 1 KiB per wave instruction.
+
+template <typename Scalar>
+__device__ __forceinline__ void load_row(const Scalar* p, Scalar* f) {
+  if constexpr (sizeof(Scalar) == 4) {
+    const uint4 v = *(const uint4*)p;
+    __builtin_memcpy(f, &v, 16);
+  } else {
+    const uint4 a = *(const uint4*)p;
+    const uint4 b = *(const uint4*)(p + 2);
+    __builtin_memcpy(f, &a, 16);
+    __builtin_memcpy(f + 2, &b, 16);
+  }
+}
+
+template <typename Scalar>
+__device__ __forceinline__ void store_row(Scalar* p, const Scalar* f) {
+  if constexpr (sizeof(Scalar) == 4) {
+    uint4 v;
+    __builtin_memcpy(&v, f, 16);
+    *(uint4*)p = v;
+  } else {
+    uint4 a, b;
+    __builtin_memcpy(&a, f, 16);
+    __builtin_memcpy(&b, f + 2, 16);
+    *(uint4*)p = a;
+    *(uint4*)(p + 2) = b;
+  }
+}
+
+struct BlockPos {
+  uint32_t ix, iy, iz;
+};
+
+template <int DIMS>
+__device__ __forceinline__ BlockPos block_pos(const Geometry& g, uint32_t b) {
+  BlockPos p;
+  if constexpr (DIMS == 1) {
+    p.ix = b; p.iy = 0; p.iz = 0;
+  } else if constexpr (DIMS == 2) {
+    p.iy = b / g.bx; p.ix = b - p.iy * g.bx; p.iz = 0;
+  } else {
+    const uint32_t plane = g.bx * g.by;
+    p.iz = b / plane;
+    const uint32_t r = b - p.iz * plane;
+    p.iy = r / g.bx;
+    p.ix = r - p.iy * g.bx;
+  }
+  return p;
+}
+
+template <typename Scalar, int DIMS, bool FAST>
+__device__ __forceinline__ void gather(const Scalar* __restrict__ data, const Geometry& g,
+                                       BlockPos bp, Scalar* f) {
+  constexpr int NY = DIMS > 1 ? 4 : 1, NZ = DIMS > 2 ? 4 : 1;
+  if constexpr (FAST) {
+    const Scalar* p = data + ((size_t)(4 * bp.iz) * g.ny + 4 * bp.iy) * g.nx + 4 * bp.ix;
+#pragma unroll
+    for (int z = 0; z < NZ; z++)
+#pragma unroll
+      for (int y = 0; y < NY; y++)
+        load_row(p + ((size_t)z * g.ny + y) * g.nx, f + 16 * z + 4 * y);
+  } else {
+    const int wx = (int)min(4u, g.nx - 4 * bp.ix);
+    const int wy = (int)min(4u, g.ny - 4 * bp.iy);
+    const int wz = (int)min(4u, g.nz - 4 * bp.iz);
+    const Scalar* p = data + (int64_t)(4 * bp.ix) * g.sx + (int64_t)(4 * bp.iy) * g.sy +
+                      (int64_t)(4 * bp.iz) * g.sz;
+#pragma unroll
+    for (int z = 0; z < NZ; z++)
+#pragma unroll
+      for (int y = 0; y < NY; y++)
+#pragma unroll
+        for (int x = 0; x < 4; x++)
+          f[16 * z + 4 * y + x] = p[(int64_t)pad_src(x, wx) * g.sx + (int64_t)pad_src(y, wy) * g.sy +
+                                    (int64_t)pad_src(z, wz) * g.sz];
+  }
+}
+
+template <typename Scalar, int DIMS, bool FAST>
+__device__ __forceinline__ void scatter(Scalar* __restrict__ data, const Geometry& g, BlockPos bp,
+                                        const Scalar* f) {
+  constexpr int NY = DIMS > 1 ? 4 : 1, NZ = DIMS > 2 ? 4 : 1;
+  if constexpr (FAST) {
+    Scalar* p = data + ((size_t)(4 * bp.iz) * g.ny + 4 * bp.iy) * g.nx + 4 * bp.ix;
+#pragma unroll
+    for (int z = 0; z < NZ; z++)
+#pragma unroll
+      for (int y = 0; y < NY; y++)
+        store_row(p + ((size_t)z * g.ny + y) * g.nx, f + 16 * z + 4 * y);
+  } else {
+    const int wx = (int)min(4u, g.nx - 4 * bp.ix);
+    const int wy = (int)min(4u, g.ny - 4 * bp.iy);
+    const int wz = (int)min(4u, g.nz - 4 * bp.iz);
+    Scalar* p = data + (int64_t)(4 * bp.ix) * g.sx + (int64_t)(4 * bp.iy) * g.sy +
+                (int64_t)(4 * bp.iz) * g.sz;
+#pragma unroll
+    for (int z = 0; z < NZ; z++)
+#pragma unroll
+      for (int y = 0; y < NY; y++)
+#pragma unroll
+        for (int x = 0; x < 4; x++)
+          if (x < wx && y < wy && z < wz)
+            p[(int64_t)x * g.sx + (int64_t)y * g.sy + (int64_t)z * g.sz] = f[16 * z + 4 * y + x];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Kernels
+
+template <typename Scalar, int DIMS, bool FAST, bool ALIGNED>
+__global__ __launch_bounds__(kLanes) void zfp_encode(const Scalar* __restrict__ data, Geometry g,
+                                                     uint64_t* __restrict__ stream) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+  constexpr int N = 1 << (2 * DIMS);
+  const uint32_t wave = g.wave0 + blockIdx.x;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t b = wave * kLanes + lane;
+  if constexpr (!ALIGNED) {
+    for (uint32_t j = lane; j < g.maxbits + 2; j += kLanes) lds[j] = 0;
+    __syncthreads();
+  }
+  if (b < g.nblocks) {
+    Scalar f[N];
+    gather<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
+    if constexpr (ALIGNED) {
+      const uint32_t W = g.maxbits >> 6;
+      LdsWordWriter wr{lds + lane * W, W, 0, 0, 0};
+      encode_block<Scalar, DIMS>(f, g.maxbits, wr);
+    } else {
+      LdsBitWriter wr{lds, lane * g.maxbits, 0, 0};
+      encode_block<Scalar, DIMS>(f, g.maxbits, wr);
+    }
+  }
+  __syncthreads();
+  const uint32_t nb = min((uint32_t)kLanes, g.nblocks - wave * kLanes);
+  const uint32_t nwords = (nb * g.maxbits + 63) >> 6;
+  uint64_t* out = stream + (size_t)wave * g.maxbits;
+  if (g.vec_io) {  // 16-byte aligned segment
+    const uint32_t npairs = nwords >> 1;
+    for (uint32_t j = lane; j < npairs; j += kLanes)
+      ((uint4*)out)[j] = ((const uint4*)lds)[j];
+    if ((nwords & 1) && lane == 0) out[nwords - 1] = lds[nwords - 1];
+  } else {
+    for (uint32_t j = lane; j < nwords; j += kLanes) out[j] = lds[j];
+  }
+}
+
+template <typename Scalar, int DIMS, bool FAST>
+__global__ __launch_bounds__(kLanes) void zfp_decode(const uint64_t* __restrict__ stream,
+                                                     Geometry g, Scalar* __restrict__ data) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+  constexpr int N = 1 << (2 * DIMS);
+  const uint32_t wave = g.wave0 + blockIdx.x;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t b = wave * kLanes + lane;
+  const uint32_t nb = min((uint32_t)kLanes, g.nblocks - wave * kLanes);
+  const uint32_t nwords = (nb * g.maxbits + 63) >> 6;
+  const uint64_t* in = stream + (size_t)wave * g.maxbits;
+  if (g.vec_io) {
+    const uint32_t npairs = nwords >> 1;
+    for (uint32_t j = lane; j < npairs; j += kLanes) ((uint4*)lds)[j] = ((const uint4*)in)[j];
+    if ((nwords & 1) && lane == 0) lds[nwords - 1] = in[nwords - 1];
+  } else {
+    for (uint32_t j = lane; j < nwords; j += kLanes) lds[j] = in[j];
+  }
+  if (lane < 2) lds[nwords + lane] = 0;  // reader look-ahead slack
+  __syncthreads();
+  if (b < g.nblocks) {
+    LdsReader rd;
+    rd.lds = lds;
+    rd.init(lane * g.maxbits);
+    Scalar f[N];
+    decode_block<Scalar, DIMS>(f, g.maxbits, rd);
+    scatter<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Launchers
+
+template <typename Scalar, int DIMS>
+int launch_encode_t(const void* data, const Geometry& g, bool fast, uint64_t* stream,
+                           uint32_t wave0, uint32_t nwaves, hipStream_t st) {
+  Geometry gg = g;
+  gg.wave0 = wave0;
+  gg.vec_io = (g.maxbits % 2 == 0) && ((uintptr_t)stream % 16 == 0);
+  const size_t lds = ((size_t)g.maxbits + 2) * 8;
+  const bool aligned = (g.maxbits & 63) == 0;
+  const Scalar* d = (const Scalar*)data;
+  if (fast && aligned)
+    hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, true, true>), dim3(nwaves), dim3(kLanes), lds, st, d, gg, stream);
+  else if (fast)
+    hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, true, false>), dim3(nwaves), dim3(kLanes), lds, st, d, gg, stream);
+  else if (aligned)
+    hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, false, true>), dim3(nwaves), dim3(kLanes), lds, st, d, gg, stream);
+  else
+    hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, false, false>), dim3(nwaves), dim3(kLanes), lds, st, d, gg, stream);
+  const hipError_t e = hipGetLastError();
+  t_last_hip = e;
+  return e == hipSuccess ? CUZFP_SUCCESS : CUZFP_ERROR_HIP;
+}
+
+template <typename Scalar, int DIMS>
+int launch_decode_t(const uint64_t* stream, const Geometry& g, bool fast, void* data,
+                           uint32_t wave0, uint32_t nwaves, hipStream_t st) {
+  Geometry gg = g;
+  gg.wave0 = wave0;
+  gg.vec_io = (g.maxbits % 2 == 0) && ((uintptr_t)stream % 16 == 0);
+  const size_t lds = ((size_t)g.maxbits + 2) * 8;
+  Scalar* d = (Scalar*)data;
+  if (fast)
+    hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, true>), dim3(nwaves), dim3(kLanes), lds, st, stream, gg, d);
+  else
+    hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, false>), dim3(nwaves), dim3(kLanes), lds, st, stream, gg, d);
+  const hipError_t e = hipGetLastError();
+  t_last_hip = e;
+  return e == hipSuccess ? CUZFP_SUCCESS : CUZFP_ERROR_HIP;
+}
+
+
+// Per-type entry points (declared in launch.hpp).
+template <typename Scalar>
+int launch_encode_type(const Problem& p, const void* data, bool fast, uint64_t* stream,
+                       uint32_t wave0, uint32_t nwaves, hipStream_t st) {
+  switch (p.dims) {
+    case 1: return launch_encode_t<Scalar, 1>(data, p.g, fast, stream, wave0, nwaves, st);
+    case 2: return launch_encode_t<Scalar, 2>(data, p.g, fast, stream, wave0, nwaves, st);
+    default: return launch_encode_t<Scalar, 3>(data, p.g, fast, stream, wave0, nwaves, st);
+  }
+}
+
+template <typename Scalar>
+int launch_decode_type(const Problem& p, const uint64_t* stream, bool fast, void* data,
+                       uint32_t wave0, uint32_t nwaves, hipStream_t st) {
+  switch (p.dims) {
+    case 1: return launch_decode_t<Scalar, 1>(stream, p.g, fast, data, wave0, nwaves, st);
+    case 2: return launch_decode_t<Scalar, 2>(stream, p.g, fast, data, wave0, nwaves, st);
+    default: return launch_decode_t<Scalar, 3>(stream, p.g, fast, data, wave0, nwaves, st);
+  }
+}
+
+}  // namespace cuzfp

@@ -1,0 +1,580 @@
+// cuzfp_amd/csrc/zfp_block.hpp -- per-block zfp fixed-rate codec, one block per lane.
+//
+// This header is the arithmetic of the MI355X codec: everything a single lane
+// does to turn one 4^d block of scalars into `maxbits` stream bits and back.
+// The HIP kernels (codec_kernels.hip) wrap it with coalesced HBM gathers and an
+// LDS-staged bitstream; tests/emulate.cpp runs the very same functions on the
+// host so the per-lane algorithm is checked against the CPU oracle without a GPU.
+//
+// Layout of one lane's work (reference: zfp 0.5.0, the ground truth of cuZFP's
+// differential harness src/utils/test.py:68-93; paths below are relative to
+// src/thirdparty_builtin/zfp-0.5.0/src):
+//
+//   emax  = exponent of max |x|              template/encode.c:9-33
+//   q[i]  = (Int)(2^(p-2-emax) * x[i])       encode.c:35-52  (p = 32 / 64)
+//   fwd_xform: lifting along x, y, z         encode.c:76-103, encode3.c:303-320
+//   u[i]  = negabinary(q[perm[i]])           encode.c:105-119, codec3.c:3-88
+//   planes = bit-matrix transpose of u        (replaces the per-plane gather
+//                                              loop of encode.c:136-138)
+//   embedded plane coder, budget-truncated   encode.c:121-151
+//
+// What is different from the reference GPU code (src/cuZFP/encode3.cuh): there a
+// 64-thread CTA cooperates on one block and thread 0 serially concatenates the
+// planes (encode3.cuh:336-362); here one lane owns the block end to end, so
+// there are no barriers, no atomics on shared words and no idle threads, and
+// the bit-plane transpose costs ~8 VALU ops per value instead of 64.
+#pragma once
+
+#include <math.h>
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define ZFP_HD __host__ __device__ __forceinline__
+#else
+#define ZFP_HD inline
+#endif
+
+namespace cuzfp {
+
+// ---------------------------------------------------------------------------
+// Scalar traits (zfp-0.5.0/src/traitsf.h, traitsd.h; cuZFP type_info.cuh:6-58)
+
+template <typename T> struct traits;
+template <> struct traits<float> {
+  typedef int32_t Int; typedef uint32_t UInt;
+  static constexpr bool is_int = false;
+  static constexpr int prec = 32, ebits = 8, ebias = 127;
+};
+template <> struct traits<double> {
+  typedef int64_t Int; typedef uint64_t UInt;
+  static constexpr bool is_int = false;
+  static constexpr int prec = 64, ebits = 11, ebias = 1023;
+};
+template <> struct traits<int32_t> {
+  typedef int32_t Int; typedef uint32_t UInt;
+  static constexpr bool is_int = true;
+  static constexpr int prec = 32, ebits = 0, ebias = 0;
+};
+template <> struct traits<int64_t> {
+  typedef int64_t Int; typedef uint64_t UInt;
+  static constexpr bool is_int = true;
+  static constexpr int prec = 64, ebits = 0, ebias = 0;
+};
+
+template <typename UInt> struct nbmask;
+template <> struct nbmask<uint32_t> { static constexpr uint32_t value = 0xaaaaaaaau; };
+template <> struct nbmask<uint64_t> { static constexpr uint64_t value = 0xaaaaaaaaaaaaaaaaull; };
+
+ZFP_HD uint64_t lowmask(unsigned n) { return n >= 64 ? ~0ull : ((1ull << n) - 1); }
+
+ZFP_HD unsigned ctz64(uint64_t x) { return (unsigned)__builtin_ctzll(x); }  // x != 0
+
+ZFP_HD unsigned umin(unsigned a, unsigned b) { return a < b ? a : b; }
+
+// ---------------------------------------------------------------------------
+// Coefficient order (zfp-0.5.0/src/template/codec{1,2,3}.c; the same tables
+// cuZFP uploads to __constant__ memory, constants.h:8-131).  Indices are used
+// only with compile-time positions, so after unrolling a permutation is pure
+// register renaming.
+
+template <int DIMS> struct perm;
+template <> struct perm<1> {
+  ZFP_HD static constexpr int at(int i) { return i; }
+};
+template <> struct perm<2> {
+  ZFP_HD static constexpr int at(int i) {
+    // (i,j) ordered by i+j, then i^2+j^2 (codec2.c:3-27)
+    return i == 0 ? 0 : i == 1 ? 1 : i == 2 ? 4 : i == 3 ? 5 : i == 4 ? 2 : i == 5 ? 8 :
+           i == 6 ? 6 : i == 7 ? 9 : i == 8 ? 3 : i == 9 ? 12 : i == 10 ? 10 : i == 11 ? 7 :
+           i == 12 ? 13 : i == 13 ? 11 : i == 14 ? 14 : 15;
+  }
+};
+#define ZFP_I3(i, j, k) ((i) + 4 * ((j) + 4 * (k)))
+template <> struct perm<3> {
+  ZFP_HD static constexpr int at(int i) {
+    // (i,j,k) ordered by i+j+k, then i^2+j^2+k^2 (codec3.c:3-88)
+    constexpr int t[64] = {
+      ZFP_I3(0,0,0),
+      ZFP_I3(1,0,0), ZFP_I3(0,1,0), ZFP_I3(0,0,1),
+      ZFP_I3(0,1,1), ZFP_I3(1,0,1), ZFP_I3(1,1,0),
+      ZFP_I3(2,0,0), ZFP_I3(0,2,0), ZFP_I3(0,0,2),
+      ZFP_I3(1,1,1),
+      ZFP_I3(2,1,0), ZFP_I3(2,0,1), ZFP_I3(0,2,1), ZFP_I3(1,2,0), ZFP_I3(1,0,2), ZFP_I3(0,1,2),
+      ZFP_I3(3,0,0), ZFP_I3(0,3,0), ZFP_I3(0,0,3),
+      ZFP_I3(2,1,1), ZFP_I3(1,2,1), ZFP_I3(1,1,2),
+      ZFP_I3(0,2,2), ZFP_I3(2,0,2), ZFP_I3(2,2,0),
+      ZFP_I3(3,1,0), ZFP_I3(3,0,1), ZFP_I3(0,3,1), ZFP_I3(1,3,0), ZFP_I3(1,0,3), ZFP_I3(0,1,3),
+      ZFP_I3(1,2,2), ZFP_I3(2,1,2), ZFP_I3(2,2,1),
+      ZFP_I3(3,1,1), ZFP_I3(1,3,1), ZFP_I3(1,1,3),
+      ZFP_I3(3,2,0), ZFP_I3(3,0,2), ZFP_I3(0,3,2), ZFP_I3(2,3,0), ZFP_I3(2,0,3), ZFP_I3(0,2,3),
+      ZFP_I3(2,2,2),
+      ZFP_I3(3,2,1), ZFP_I3(3,1,2), ZFP_I3(1,3,2), ZFP_I3(2,3,1), ZFP_I3(2,1,3), ZFP_I3(1,2,3),
+      ZFP_I3(0,3,3), ZFP_I3(3,0,3), ZFP_I3(3,3,0),
+      ZFP_I3(3,2,2), ZFP_I3(2,3,2), ZFP_I3(2,2,3),
+      ZFP_I3(1,3,3), ZFP_I3(3,1,3), ZFP_I3(3,3,1),
+      ZFP_I3(2,3,3), ZFP_I3(3,2,3), ZFP_I3(3,3,2),
+      ZFP_I3(3,3,3)};
+    return t[i];
+  }
+};
+#undef ZFP_I3
+
+// Permutation with the table index as a template constant (no runtime-indexed
+// register array, hence no scratch): u[i] = negabinary(q[perm[i]]) and back.
+template <int... I> struct seq {};
+template <int N, int... I> struct seq_gen : seq_gen<N - 1, N - 1, I...> {};
+template <int... I> struct seq_gen<0, I...> { typedef seq<I...> type; };
+template <int N> using make_seq = typename seq_gen<N>::type;
+template <int DIMS, int I> struct pidx { static constexpr int value = perm<DIMS>::at(I); };
+
+template <int DIMS, typename UInt, int... I>
+ZFP_HD void permute_fwd(const UInt* q, UInt* u, UInt nb, seq<I...>) {
+  ((u[I] = (q[pidx<DIMS, I>::value] + nb) ^ nb), ...);
+}
+template <int DIMS, typename UInt, int... I>
+ZFP_HD void permute_inv(const UInt* u, UInt* q, UInt nb, seq<I...>) {
+  ((q[pidx<DIMS, I>::value] = (u[I] ^ nb) - nb), ...);
+}
+
+// precision() (codec1.c:8-11, codec2.c:131-136, codec3.c:92-97): planes coded
+// for a block with exponent emax in fixed-rate mode (maxprec = type precision,
+// minexp = ZFP_MIN_EXP = -1074).
+template <int DIMS>
+ZFP_HD unsigned precision(int emax, int prec) {
+  int p = emax + 1074 + 2 * (DIMS + 1);
+  p = p < 0 ? 0 : p;
+  return (unsigned)(p < prec ? p : prec);
+}
+
+// ---------------------------------------------------------------------------
+// Lifting transform (encode.c:76-103 / decode.c:243-270) on the unsigned type,
+// so the reference's wrap-around (x86 int arithmetic) is well defined here.
+
+ZFP_HD uint32_t asr1(uint32_t v) { return (uint32_t)((int32_t)v >> 1); }
+ZFP_HD uint64_t asr1(uint64_t v) { return (uint64_t)((int64_t)v >> 1); }
+
+template <typename UInt>
+ZFP_HD void fwd_lift(UInt& x, UInt& y, UInt& z, UInt& w) {
+  x += w; x = asr1(x); w -= x;
+  z += y; z = asr1(z); y -= z;
+  x += z; x = asr1(x); z -= x;
+  w += y; w = asr1(w); y -= w;
+  w += asr1(y); y -= asr1(w);
+}
+
+template <typename UInt>
+ZFP_HD void inv_lift(UInt& x, UInt& y, UInt& z, UInt& w) {
+  y += asr1(w); w -= asr1(y);
+  y += w; w <<= 1; w -= y;
+  z += x; x <<= 1; x -= z;
+  y += z; z <<= 1; z -= y;
+  w += x; x <<= 1; x -= w;
+}
+
+template <int DIMS, typename UInt>
+ZFP_HD void fwd_xform(UInt* p) {
+  if constexpr (DIMS == 1) {
+    fwd_lift(p[0], p[1], p[2], p[3]);
+  } else if constexpr (DIMS == 2) {
+#pragma unroll
+    for (int y = 0; y < 4; y++) fwd_lift(p[4 * y], p[4 * y + 1], p[4 * y + 2], p[4 * y + 3]);
+#pragma unroll
+    for (int x = 0; x < 4; x++) fwd_lift(p[x], p[x + 4], p[x + 8], p[x + 12]);
+  } else {
+#pragma unroll
+    for (int zy = 0; zy < 16; zy++) fwd_lift(p[4 * zy], p[4 * zy + 1], p[4 * zy + 2], p[4 * zy + 3]);
+#pragma unroll
+    for (int z = 0; z < 4; z++)
+#pragma unroll
+      for (int x = 0; x < 4; x++) {
+        UInt* q = p + 16 * z + x;
+        fwd_lift(q[0], q[4], q[8], q[12]);
+      }
+#pragma unroll
+    for (int yx = 0; yx < 16; yx++) fwd_lift(p[yx], p[yx + 16], p[yx + 32], p[yx + 48]);
+  }
+}
+
+template <int DIMS, typename UInt>
+ZFP_HD void inv_xform(UInt* p) {
+  if constexpr (DIMS == 1) {
+    inv_lift(p[0], p[1], p[2], p[3]);
+  } else if constexpr (DIMS == 2) {
+#pragma unroll
+    for (int x = 0; x < 4; x++) inv_lift(p[x], p[x + 4], p[x + 8], p[x + 12]);
+#pragma unroll
+    for (int y = 0; y < 4; y++) inv_lift(p[4 * y], p[4 * y + 1], p[4 * y + 2], p[4 * y + 3]);
+  } else {
+#pragma unroll
+    for (int yx = 0; yx < 16; yx++) inv_lift(p[yx], p[yx + 16], p[yx + 32], p[yx + 48]);
+#pragma unroll
+    for (int z = 0; z < 4; z++)
+#pragma unroll
+      for (int x = 0; x < 4; x++) {
+        UInt* q = p + 16 * z + x;
+        inv_lift(q[0], q[4], q[8], q[12]);
+      }
+#pragma unroll
+    for (int zy = 0; zy < 16; zy++) inv_lift(p[4 * zy], p[4 * zy + 1], p[4 * zy + 2], p[4 * zy + 3]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Bit-plane transpose.  R rows of 32-bit words are cut into 32/R square R x R
+// tiles side by side; each tile is transposed in place by log2(R) butterfly
+// stages of bit-field inserts.  Afterwards word j holds, in bits [R*s, R*s+R),
+// column R*s + j of the input, i.e. plane (R*s + j) of R coefficients.  The
+// operation is an involution, so the decoder uses it unchanged.
+
+template <int J>
+ZFP_HD void transpose_stage(uint32_t* a, int rows) {
+  // swap the J x J off-diagonal sub-blocks of every 2J x 2J tile
+  constexpr uint32_t m = J == 16 ? 0x0000ffffu : J == 8 ? 0x00ff00ffu : J == 4 ? 0x0f0f0f0fu
+                       : J == 2 ? 0x33333333u : 0x55555555u;
+#pragma unroll
+  for (int i = 0; i < 32; i++) {
+    if (i >= rows || (i & J)) continue;
+    const uint32_t lo = a[i], hi = a[i + J];
+    a[i] = (lo & m) | ((hi << J) & ~m);      // v_bfi_b32
+    a[i + J] = ((lo >> J) & m) | (hi & ~m);  // v_bfi_b32
+  }
+}
+
+template <int R>
+ZFP_HD void transpose_tiles(uint32_t* a) {
+  // stages J = R/2, ..., 1 spelled out so every index is a compile-time constant
+  if constexpr (R >= 32) transpose_stage<16>(a, R);
+  if constexpr (R >= 16) transpose_stage<8>(a, R);
+  if constexpr (R >= 8) transpose_stage<4>(a, R);
+  if constexpr (R >= 4) transpose_stage<2>(a, R);
+  if constexpr (R >= 2) transpose_stage<1>(a, R);
+}
+
+// Planes of N = 4^DIMS coefficients held as 32-bit words.  For 32-bit
+// coefficients W = N words; 64-bit coefficients are split into low and high
+// halves (planes 0..31 from the low words, 32..63 from the high words).
+template <typename UInt, int DIMS> struct planes {
+  static constexpr int N = 1 << (2 * DIMS);
+  static constexpr int H = sizeof(UInt) / 4;      // 32-bit halves per value
+  static constexpr int R = N < 32 ? N : 32;       // tile height
+  static constexpr int G = N / R;                 // row groups (2 for 3D)
+  uint32_t w[H][N];                               // w[half][group*R + row]
+
+  ZFP_HD void load(const UInt* u) {
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      w[0][i] = (uint32_t)u[i];
+      if (H == 2) w[H - 1][i] = (uint32_t)((uint64_t)u[i] >> 32);
+    }
+#pragma unroll
+    for (int h = 0; h < H; h++)
+#pragma unroll
+      for (int g = 0; g < G; g++) transpose_tiles<R>(&w[h][g * R]);
+  }
+
+  ZFP_HD void store(UInt* u) {
+#pragma unroll
+    for (int h = 0; h < H; h++)
+#pragma unroll
+      for (int g = 0; g < G; g++) transpose_tiles<R>(&w[h][g * R]);
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      uint64_t v = w[0][i];
+      if (H == 2) v |= (uint64_t)w[H - 1][i] << 32;
+      u[i] = (UInt)v;
+    }
+  }
+
+  // plane k as an N-bit word (bit i = bit k of coefficient i); k compile-time
+  // after unrolling.
+  ZFP_HD uint64_t get(int k) const {
+    const int h = k >> 5, c = k & 31;
+    if (N == 64) return (uint64_t)w[h][c] | ((uint64_t)w[h][32 + c] << 32);
+    return (w[h][c % R] >> (R * (c / R))) & (uint32_t)lowmask(R);
+  }
+
+  ZFP_HD void zero() {
+#pragma unroll
+    for (int h = 0; h < H; h++)
+#pragma unroll
+      for (int i = 0; i < N; i++) w[h][i] = 0;
+  }
+
+  // deposit plane k (bits beyond N are zero)
+  ZFP_HD void set(int k, uint64_t x) {
+    const int h = k >> 5, c = k & 31;
+    if (N == 64) {
+      w[h][c] = (uint32_t)x;
+      w[h][32 + c] = (uint32_t)(x >> 32);
+    } else {
+      w[h][c % R] |= (uint32_t)x << (R * (c / R));
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Embedded plane coder with a bit budget (encode.c:121-151).  Per plane k,
+// most significant first: the first n bits verbatim (coefficients already
+// significant), then group tests: "1" + the bits up to and including the next
+// one bit (the one at position N-1 is implied), until a "0" test or the end of
+// the plane.  Each group is emitted with one writer call; a call that would
+// overrun the budget is cut to the remaining bits, which makes the output
+// exactly the reference's prefix.
+
+// The plane loop is unrolled by template recursion so that plane K is a
+// compile-time register index (a runtime-indexed plane array would live in
+// scratch memory).  A lane that runs out of budget returns; the wave walks on
+// only while some lane still has bits left.
+template <int K, typename UInt, int DIMS, typename Writer>
+ZFP_HD void encode_planes_from(const planes<UInt, DIMS>& P, unsigned& bits, unsigned& n, int kmin,
+                               Writer& wr) {
+  if constexpr (K >= 0) {
+    constexpr unsigned N = 1u << (2 * DIMS);
+    if (!bits || K < kmin) return;
+    const uint64_t x = P.get(K);
+    // verbatim part: the n coefficients already known to be significant
+    const unsigned m = umin(n, bits);
+    wr.put(x & lowmask(m), m);
+    bits -= m;
+    uint64_t r = n < N ? x >> n : 0;
+    while (n < N && bits) {
+      if (!r) {  // group test fails: plane done
+        wr.put(0, 1);
+        bits--;
+        break;
+      }
+      const unsigned z = ctz64(r);
+      const unsigned p = n + z;
+      const bool last = p == N - 1;
+      unsigned len = z + (last ? 1u : 2u);
+      uint64_t code = last ? 1ull : (1ull | (2ull << z));
+      if (len > bits) {
+        len = bits;
+        code &= lowmask(len);
+      }
+      wr.put(code, len);
+      bits -= len;
+      n = p + 1;
+      r = (z < 63) ? r >> (z + 1) : 0;
+    }
+    encode_planes_from<K - 1, UInt, DIMS>(P, bits, n, kmin, wr);
+  }
+}
+
+template <typename UInt, int DIMS, typename Writer>
+ZFP_HD void encode_planes(const planes<UInt, DIMS>& P, unsigned budget, unsigned maxprec,
+                          Writer& wr) {
+  constexpr int PREC = (int)sizeof(UInt) * 8;
+  const int kmin = PREC > (int)maxprec ? PREC - (int)maxprec : 0;
+  unsigned bits = budget, n = 0;
+  encode_planes_from<PREC - 1, UInt, DIMS>(P, bits, n, kmin, wr);
+}
+
+// decode.c:288-321.  Runs of zeros are skipped with one count-trailing-zeros
+// on a 64-bit window; when the budget ends inside a run the reference still
+// deposits a one at the current position, and so do we.
+template <int K, typename UInt, int DIMS, typename Reader>
+ZFP_HD void decode_planes_from(planes<UInt, DIMS>& P, unsigned& bits, unsigned& n, int kmin,
+                               Reader& rd) {
+  if constexpr (K >= 0) {
+    constexpr unsigned N = 1u << (2 * DIMS);
+    if (!bits || K < kmin) return;
+    const unsigned m = umin(n, bits);
+    uint64_t x = rd.peek() & lowmask(m);
+    rd.skip(m);
+    bits -= m;
+    while (n < N && bits) {
+      const uint64_t wnd = rd.peek();
+      bits--;
+      if (!(wnd & 1)) {
+        rd.skip(1);
+        break;
+      }
+      const unsigned lim = umin(N - 1 - n, bits);
+      const uint64_t rest = wnd >> 1;
+      const unsigned z = rest ? ctz64(rest) : 64u;
+      unsigned adv;
+      if (z < lim) {
+        adv = z + 1;
+        n += z;
+      } else {
+        adv = lim;
+        n += lim;
+      }
+      rd.skip(1 + adv);
+      bits -= adv;
+      x |= 1ull << n;
+      n++;
+    }
+    P.set(K, x);
+    decode_planes_from<K - 1, UInt, DIMS>(P, bits, n, kmin, rd);
+  }
+}
+
+template <typename UInt, int DIMS, typename Reader>
+ZFP_HD void decode_planes(planes<UInt, DIMS>& P, unsigned budget, unsigned maxprec, Reader& rd) {
+  constexpr int PREC = (int)sizeof(UInt) * 8;
+  const int kmin = PREC > (int)maxprec ? PREC - (int)maxprec : 0;
+  unsigned bits = budget, n = 0;
+  P.zero();
+  decode_planes_from<PREC - 1, UInt, DIMS>(P, bits, n, kmin, rd);
+}
+
+// ---------------------------------------------------------------------------
+// Block exponent and the float <-> int casts.
+
+template <typename Scalar> struct fp;
+
+template <> struct fp<float> {
+  // exponent of max |x| (encode.c:9-33): frexp exponent, clamped to -126 for
+  // denormals, -127 for an all-zero block; frexp(inf) gives 0 (glibc).  fmaxf
+  // ignores NaNs exactly as the reference's `if (max < f)` loop does.
+  template <int N>
+  ZFP_HD static int emax(const float* f) {
+    float m = 0.0f;
+#pragma unroll
+    for (int i = 0; i < N; i++) m = fmaxf(m, fabsf(f[i]));
+    uint32_t b = __float_as_uint_(m);
+    int E = (int)(b >> 23);
+    if (b == 0) return -127;
+    return E == 255 ? 0 : E - 126;
+  }
+  // 2^e as a float, e in [-160, 160], with IEEE underflow / overflow
+  ZFP_HD static float pow2(int e) {
+    if (e > 127) return __uint_as_float_(0x7f800000u);
+    if (e >= -126) return __uint_as_float_((uint32_t)(e + 127) << 23);
+    if (e >= -149) return __uint_as_float_(1u << (e + 149));
+    return 0.0f;  // 2^-150 rounds (to even) to zero, like ldexpf
+  }
+  // (Int)(s * x) with x86-64 cvttss2si semantics: NaN or |y| >= 2^31 -> INT_MIN
+  ZFP_HD static int32_t to_int(float y) {
+    return fabsf(y) < 2147483648.0f ? (int32_t)y : (int32_t)0x80000000u;
+  }
+  ZFP_HD static float from_int(int32_t q) { return (float)q; }
+  ZFP_HD static uint32_t __float_as_uint_(float f) { union { float f; uint32_t u; } c; c.f = f; return c.u; }
+  ZFP_HD static float __uint_as_float_(uint32_t u) { union { float f; uint32_t u; } c; c.u = u; return c.f; }
+};
+
+template <> struct fp<double> {
+  template <int N>
+  ZFP_HD static int emax(const double* f) {
+    double m = 0.0;
+#pragma unroll
+    for (int i = 0; i < N; i++) m = fmax(m, fabs(f[i]));
+    uint64_t b = as_u64(m);
+    int E = (int)(b >> 52);
+    if (b == 0) return -1023;
+    return E == 2047 ? 0 : E - 1022;
+  }
+  ZFP_HD static double pow2(int e) {
+    if (e > 1023) return as_f64(0x7ff0000000000000ull);
+    if (e >= -1022) return as_f64((uint64_t)(e + 1023) << 52);
+    if (e >= -1074) return as_f64(1ull << (e + 1074));
+    return 0.0;
+  }
+  ZFP_HD static int64_t to_int(double y) {
+    return fabs(y) < 9223372036854775808.0 ? (int64_t)y : (int64_t)0x8000000000000000ull;
+  }
+  ZFP_HD static double from_int(int64_t q) { return (double)q; }
+  ZFP_HD static uint64_t as_u64(double f) { union { double f; uint64_t u; } c; c.f = f; return c.u; }
+  ZFP_HD static double as_f64(uint64_t u) { union { double f; uint64_t u; } c; c.u = u; return c.f; }
+};
+
+// ---------------------------------------------------------------------------
+// Whole-block encode / decode.  Writer: put(value, n) appends n <= 64 low bits
+// (value has no bits at or above n); finish() pads the block to maxbits.
+// Reader: peek() returns the next 64 stream bits, skip(n) consumes n <= 64.
+
+template <typename Scalar, int DIMS, typename Writer>
+ZFP_HD void encode_block(const Scalar* f, unsigned maxbits, Writer& wr) {
+  typedef traits<Scalar> T;
+  typedef typename T::Int Int;
+  typedef typename T::UInt UInt;
+  constexpr int N = 1 << (2 * DIMS);
+  UInt q[N];
+  unsigned budget = maxbits, maxprec = T::prec;
+  if constexpr (!T::is_int) {
+    // encode.c:187-216
+    const int emax = fp<Scalar>::template emax<N>((const Scalar*)f);
+    maxprec = precision<DIMS>(emax, T::prec);
+    const unsigned e = maxprec ? (unsigned)(emax + T::ebias) : 0u;
+    if (!e) {  // all-zero block: a single 0 bit, then padding
+      wr.put(0, 1);
+      wr.finish();
+      return;
+    }
+    wr.put(2ull * e + 1, T::ebits + 1);
+    budget = maxbits - (T::ebits + 1);
+    const int sh = T::prec - 2 - emax;
+    if (sh > (T::prec == 32 ? 127 : 1023)) {
+      // scale factor overflows to +inf: every product is +-inf or NaN, which the
+      // reference's x86 cast turns into INT_MIN (see oracle/zfp_oracle.c)
+#pragma unroll
+      for (int i = 0; i < N; i++) q[i] = (UInt)1 << (T::prec - 1);
+    } else {
+      const Scalar s = (Scalar)fp<Scalar>::pow2(sh);
+#pragma unroll
+      for (int i = 0; i < N; i++) q[i] = (UInt)fp<Scalar>::to_int(s * (Scalar)f[i]);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; i++) q[i] = (UInt)(Int)f[i];
+  }
+  fwd_xform<DIMS>(q);
+  UInt u[N];
+  constexpr UInt NB = nbmask<UInt>::value;
+  permute_fwd<DIMS>(q, u, NB, make_seq<N>());
+  planes<UInt, DIMS> P;
+  P.load(u);
+  encode_planes<UInt, DIMS>(P, budget, maxprec, wr);
+  wr.finish();
+}
+
+template <typename Scalar, int DIMS, typename Reader>
+ZFP_HD void decode_block(Scalar* f, unsigned maxbits, Reader& rd) {
+  typedef traits<Scalar> T;
+  typedef typename T::Int Int;
+  typedef typename T::UInt UInt;
+  constexpr int N = 1 << (2 * DIMS);
+  unsigned budget = maxbits, maxprec = T::prec;
+  int emax = 0;
+  if constexpr (!T::is_int) {
+    // decode.c:352-381
+    const uint64_t head = rd.peek();
+    if (!(head & 1)) {
+#pragma unroll
+      for (int i = 0; i < N; i++) f[i] = (Scalar)0;
+      return;
+    }
+    emax = (int)((head >> 1) & lowmask(T::ebits)) - T::ebias;
+    rd.skip(T::ebits + 1);
+    maxprec = precision<DIMS>(emax, T::prec);
+    budget = maxbits - (T::ebits + 1);
+  }
+  planes<UInt, DIMS> P;
+  decode_planes<UInt, DIMS>(P, budget, maxprec, rd);
+  UInt u[N];
+  P.store(u);
+  UInt q[N];
+  constexpr UInt NB = nbmask<UInt>::value;
+  permute_inv<DIMS>(u, q, NB, make_seq<N>());
+  inv_xform<DIMS>(q);
+  if constexpr (!T::is_int) {
+    const Scalar s = (Scalar)fp<Scalar>::pow2(emax - (T::prec - 2));
+#pragma unroll
+    for (int i = 0; i < N; i++) f[i] = (Scalar)(s * (Scalar)(Int)q[i]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; i++) f[i] = (Scalar)(Int)q[i];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Partial-block padding (encode.c:54-74 pad_block, applied along x, y, z by
+// encode3.c:284-301).  It is separable: padded index i of an edge with n valid
+// values reads source index pad_src(i, n).
+
+ZFP_HD int pad_src(int i, int n) { return i < n ? i : (i == 3 ? 0 : n - 1); }
+
+}  // namespace cuzfp

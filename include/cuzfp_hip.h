@@ -1,0 +1,111 @@
+/*
+ * include/cuzfp_hip.h -- C-ABI of the MI355X-native zfp fixed-rate codec.
+ *
+ * This is the drop-in boundary: plain pointers, sizes and a HIP stream, no C++
+ * or torch types.  The C++ surface of the reference (`cuZFP::compress`,
+ * `cuZFP::decompress`, include/cuZFP.h) is implemented on top of it
+ * (cuzfp_amd/csrc/cuZFP.cpp); Python, ctypes, cgo or JNI callers bind it
+ * directly.
+ *
+ * Each entry point names the reference interface it replaces (paths relative to
+ * /root/reference/src/cuZFP):
+ *
+ *   cuzfp_hip_encode  <- internal::encode<T>(dims, maxbits, d_data, d_stream)
+ *                        cuZFP.cu:26-64, i.e. encode1launch / encode2launch /
+ *                        encode3launch (encode1.cuh:458-526, encode2.cuh:462-528,
+ *                        encode3.cuh:428-508) and their kernels.
+ *   cuzfp_hip_decode  <- internal::decode<T>(dims, maxbits, d_stream, d_data)
+ *                        cuZFP.cu:66-105 -> decode{1,2,3}launch (decode1.cuh:102-145,
+ *                        decode2.cuh:141-182, decode3.cuh:217-264).
+ *   cuzfp_hip_stream_bytes <- the byte count those launchers return
+ *                        (calc_device_mem{1,2,3}d, e.g. encode3.cuh:413-423).
+ *   cuzfp_hip_maximum_size <- zfp_stream_maximum_size (zfp_structs.h:237-266).
+ *   cuzfp_hip_rate_to_maxbits <- stream_set_rate (zfp_structs.h:61-91).
+ *   cuzfp_hip_compress_host / cuzfp_hip_decompress_host <- the host-pointer
+ *                        staging of cuZFP::compress / decompress
+ *                        (cuZFP.cu:107-170, 174-269), as a pinned, chunked,
+ *                        stream-overlapped pipeline.
+ *
+ * Stream format: bit-exact with zfp 0.5.0 fixed-rate mode (the ground truth of
+ * the reference's src/utils/test.py:68-93): 64-bit little-endian words, bits
+ * LSB first, block b (raster order z, y, x) at bits [b*maxbits, (b+1)*maxbits),
+ * zero padded to a whole word; no header.
+ *
+ * Unlike the reference (cuZFP.cu:174-269: errors printed, execution continues),
+ * every call returns a cuzfp_status.  Device calls are asynchronous on
+ * `stream` (0 = the null stream) and never allocate or synchronise, so they
+ * can be captured into a hipGraph.
+ */
+#ifndef CUZFP_HIP_H
+#define CUZFP_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CUZFP_HIP_ABI_VERSION 1
+
+/* scalar type codes: the reference's zfp_type enum (zfp_structs.h:46-52) */
+#define CUZFP_TYPE_INT32 1
+#define CUZFP_TYPE_INT64 2
+#define CUZFP_TYPE_FLOAT 3
+#define CUZFP_TYPE_DOUBLE 4
+
+typedef enum {
+  CUZFP_SUCCESS = 0,
+  CUZFP_ERROR_INVALID_ARGUMENT = 1, /* bad dims, maxbits or null pointer   */
+  CUZFP_ERROR_UNSUPPORTED_TYPE = 2, /* type code not 1..4                   */
+  CUZFP_ERROR_BUFFER_TOO_SMALL = 3, /* stream capacity < needed bytes       */
+  CUZFP_ERROR_HIP = 4               /* a HIP runtime call failed            */
+} cuzfp_status;
+
+int cuzfp_hip_abi_version(void);
+const char* cuzfp_hip_status_string(int status);
+/* last HIP error seen by this thread (hipSuccess if none) */
+int cuzfp_hip_last_hip_error(void);
+
+/* maxbits for `rate` bits/value: floor(4^dims * rate + 0.5), at least 1 + the
+ * exponent bits (9 float, 12 double); wra != 0 rounds up to a multiple of 64,
+ * which is what the reference's stream_set_rate does for 3D arrays. */
+unsigned cuzfp_hip_rate_to_maxbits(double rate, int type, unsigned dims, int wra);
+
+/* Exact compressed size: ceil(blocks * maxbits / 64) * 8.  ny == 0 -> 1D,
+ * nz == 0 -> 2D. Returns 0 for invalid arguments. */
+size_t cuzfp_hip_stream_bytes(int type, unsigned nx, unsigned ny, unsigned nz, unsigned maxbits);
+
+/* Worst-case buffer size, the reference's zfp_stream_maximum_size. */
+size_t cuzfp_hip_maximum_size(int type, unsigned nx, unsigned ny, unsigned nz, unsigned maxbits);
+
+/* Compress a device-resident array into a device-resident stream.
+ * Strides are in elements (0 = contiguous a[nz][ny][nx]; negative allowed).
+ * *out_bytes (optional) receives cuzfp_hip_stream_bytes(). */
+int cuzfp_hip_encode(const void* d_data, int type, unsigned nx, unsigned ny, unsigned nz,
+                     long long sx, long long sy, long long sz, unsigned maxbits,
+                     uint64_t* d_stream, size_t stream_capacity, size_t* out_bytes,
+                     hipStream_t stream);
+
+/* Decompress a device-resident stream into a device-resident array. */
+int cuzfp_hip_decode(const uint64_t* d_stream, size_t stream_bytes, int type, unsigned nx,
+                     unsigned ny, unsigned nz, long long sx, long long sy, long long sz,
+                     unsigned maxbits, void* d_data, hipStream_t stream);
+
+/* Host-memory end to end: the array and the stream live in
+ * host memory; the library moves them through pinned staging buffers in
+ * z-slab (3D) / y-slab (2D) / x-range (1D) chunks on `nstreams` HIP streams so
+ * the copies overlap the kernels.  Synchronous; contiguous arrays only. */
+int cuzfp_hip_compress_host(const void* h_data, int type, unsigned nx, unsigned ny,
+                            unsigned nz, unsigned maxbits, void* h_stream,
+                            size_t stream_capacity, size_t* out_bytes, int nstreams);
+int cuzfp_hip_decompress_host(const void* h_stream, size_t stream_bytes, int type,
+                              unsigned nx, unsigned ny, unsigned nz, unsigned maxbits,
+                              void* h_data, int nstreams);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
