@@ -1,0 +1,298 @@
+"""Benchmark: zfp fixed-rate encode+decode, device-resident, on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...     (one process per GPU)
+
+A step is one pass of the hot path over one batch: encode the rank's array
+into its fixed-rate stream, then decode the stream back, both on the GPU with
+the data already in HBM.  Workload (BASELINE.json configs[1]): a 256^3 float32
+array at 8 bits/value (maxbits 512) per GPU, filled with testzfp's polynomial
+field (zfp-0.5.0/tests/testzfp.cpp:33-72).  With N GPUs every rank owns one
+256^3 z-slab of a 256 x 256 x 256N array (weak scaling; blocks are independent,
+so there is no collective on the data path).  The compressed-stream all-gather
+over RCCL (the north star's exchange step) is timed separately, after the
+timed region, and reported under "allgather".
+
+Prints one JSON line on rank 0 (the driver contract), with
+  value       = input GB/s of all ranks (10^9 B of input / s)
+  roofline    = the dominant kernel's algorithmic bytes / its mean duration,
+                over the MI355X HBM3E peak (8.0 TB/s, MI355X_MICROARCH.md)
+  cpu_baseline= the reference's own CPU zfp 0.5.0 (oracle/_ref), timed here.
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "GB/s input encoded+decoded (device-resident), 3D f32 fixed-rate; % HBM peak"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--size", type=int, default=256, help="per-GPU cube edge (3D)")
+    p.add_argument("--rate", type=float, default=8.0)
+    p.add_argument("--dtype", default="float32", choices=["float32", "float64"])
+    p.add_argument("--field", default="polynomial", choices=["polynomial", "splitmix"])
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-host-path", action="store_true")
+    p.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    return p.parse_args()
+
+
+def cpu_baseline(a: np.ndarray, maxbits: int):
+    """Reference CPU zfp 0.5.0 (zfp_compress + zfp_decompress), slab-parallel over
+    this process's cores, on the first 64 z-planes of the workload (a bounded
+    sample: 1/4 of the 256^3 array)."""
+    try:
+        import oracle
+    except Exception:  # pragma: no cover
+        return None
+    ref = oracle.reference
+    kind = "reference"
+    if ref is None:
+        return None
+    sample = np.ascontiguousarray(a[:64])
+    cores = max(1, min(16, len(os.sched_getaffinity(0))))
+    reps = 5
+    t0 = time.perf_counter()
+    rt, enc, dec, _ = ref.time_roundtrip(sample, maxbits, threads=cores, reps=reps)
+    rt1, enc1, dec1, _ = ref.time_roundtrip(sample[:16], maxbits, threads=1, reps=3)
+    wall = time.perf_counter() - t0
+    nbytes = sample.nbytes
+    return {"value": round(nbytes / rt / 1e9, 4), "unit": "GB/s", "cores": cores, "kind": kind,
+            "sample": f"{sample.shape[0]}x{sample.shape[1]}x{sample.shape[2]} {sample.dtype} slab of the "
+                      f"workload, maxbits {maxbits}, median of {reps} round trips, z-slab threads",
+            "encode_GBps": round(nbytes / enc / 1e9, 4), "decode_GBps": round(nbytes / dec / 1e9, 4),
+            "single_core_GBps": round(sample[:16].nbytes / rt1 / 1e9, 4),
+            "wall_s": round(wall, 2)}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import cuzfp_amd as cz
+    from cuzfp_amd import dist as zd
+    from cuzfp_amd.datagen import polynomial_slab, splitmix_uniform
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+
+    dtype = np.dtype(args.dtype)
+    n = args.size
+    shape = (n, n, n)                                  # this rank's z-slab
+    gshape = (n * world, n, n)                         # the global array
+    maxbits = cz.rate_to_maxbits(args.rate, dtype, 3)
+    # each rank's slab: planes [rank*n, (rank+1)*n) of the global field
+    if args.field == "polynomial":
+        a = polynomial_slab(gshape, rank * n, (rank + 1) * n, dtype)
+    else:
+        a = splitmix_uniform(shape, dtype, seed=42 + rank)
+    x = torch.from_numpy(a).to(dev)
+    nbytes_stream = cz.stream_bytes(shape, dtype, maxbits)
+    words = torch.empty(nbytes_stream // 8, dtype=torch.int64, device=dev)
+    y = torch.empty_like(x)
+    stream = torch.cuda.current_stream()
+
+    def step():  # launches on torch's current stream (the capture stream under a graph)
+        cz.encode(x, maxbits, out=words)
+        cz.decode(words, shape, x.dtype, maxbits, out=y)
+
+    def graphed(fn, count):
+        """`count` calls of fn captured into one hipGraph (launch overhead off the
+        host's critical path); falls back to eager calls if capture fails."""
+        if args.no_graph:
+            return lambda: [fn() for _ in range(count)]
+        try:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(count):
+                    fn()
+            return g.replay
+        except Exception as e:  # pragma: no cover
+            print(f"graph capture failed ({e}); timing eager launches", file=sys.stderr)
+            return lambda: [fn() for _ in range(count)]
+
+    # correctness of the benchmarked configuration: round-trip error within
+    # testzfp's bound for this field, and (N=1, polynomial) the stream hash of
+    # the reference's own zfp 0.5.0 output (tests/golden/golden.json)
+    step()
+    torch.cuda.synchronize()
+    max_err = float((y.double() - x.double()).abs().max().item())
+    parity = None
+    gpath = os.path.join(ROOT, "tests", "golden", "golden.json")
+    key = {("float32", 8.0): "baseline/3d_f32_256_r8", ("float64", 16.0): "baseline/3d_f64_256_r16"}.get(
+        (args.dtype, args.rate))
+    if key and n == 256 and world == 1 and os.path.exists(gpath):
+        rec = json.load(open(gpath))["cases"].get(f"{key}/{args.field}")
+        if rec:
+            got = hashlib.sha256(words.cpu().numpy().tobytes()).hexdigest()
+            parity = "stream sha256 == reference zfp 0.5.0" if got == rec["stream_sha256"] else "MISMATCH"
+
+    per_graph = next(c for c in (10, 5, 4, 2, 1) if args.steps % c == 0)
+    run = graphed(step, per_graph)
+    for _ in range(args.warmup):
+        step()
+    run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    for _ in range(args.steps // per_graph):
+        run()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    t_local = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t_local, op=dist.ReduceOp.MAX)
+    elapsed = float(t_local.item())
+    gpu_ms_per_step = ev0.elapsed_time(ev1) / args.steps
+
+    # per-kernel durations with HIP events on the launch stream
+    def time_kernel(fn, reps):
+        r = graphed(fn, 10)
+        r()
+        torch.cuda.synchronize()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps // 10):
+            r()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / (reps // 10 * 10)
+
+    reps = 10 * max(2, args.steps // 10)
+    enc_ms = time_kernel(lambda: cz.encode(x, maxbits, out=words), reps)
+    dec_ms = time_kernel(lambda: cz.decode(words, shape, x.dtype, maxbits, out=y), reps)
+
+    # optional RCCL all-gather of the compressed stream (the exchange step)
+    allgather = None
+    if world > 1 and zd.uniform_shard_ok(gshape, world, maxbits):
+        full = zd.allgather_stream(words)
+        torch.cuda.synchronize()
+        dist.barrier()
+        ag0 = time.perf_counter()
+        agr = 5
+        for _ in range(agr):
+            full = zd.allgather_stream(words)
+        torch.cuda.synchronize()
+        ag_s = (time.perf_counter() - ag0) / agr
+        t = torch.tensor([ag_s], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ag_s = float(t.item())
+        allgather = {"bytes_per_rank_in": int(full.numel() * 8 - nbytes_stream), "ms": round(ag_s * 1e3, 3),
+                     "GBps_per_rank_in": round((full.numel() * 8 - nbytes_stream) / ag_s / 1e9, 2),
+                     "backend": "nccl (RCCL)"}
+        del full
+
+    n_in = a.nbytes
+    value = n_in * world * args.steps / elapsed / 1e9
+    s_bytes = nbytes_stream
+    enc_bytes = n_in + s_bytes     # read array, write stream
+    dec_bytes = s_bytes + n_in     # read stream, write array
+    dominant = "encode" if enc_ms >= dec_ms else "decode"
+    dom_ms = max(enc_ms, dec_ms)
+    dom_bytes = enc_bytes if dominant == "encode" else dec_bytes
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            wk = f"3d_{args.dtype}_{n}^3_rate{args.rate:g}"
+            if tj.get("workload") == wk:
+                traffic = tj.get(dominant + "_hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    result = None
+    if rank == 0:
+        host_path = None
+        if world == 1 and not args.no_host_path:
+            hp_in = torch.from_numpy(a).pin_memory().numpy()
+            hp_out = torch.empty(s_bytes // 8, dtype=torch.int64).pin_memory().numpy().view(np.uint64)
+            hp_back = torch.empty(a.shape, dtype=x.dtype).pin_memory().numpy()
+            cz.compress_host(hp_in, maxbits, out=hp_out)
+            cz.decompress_host(hp_out, shape, dtype, maxbits, out=hp_back)
+            tc = time.perf_counter()
+            for _ in range(5):
+                cz.compress_host(hp_in, maxbits, out=hp_out)
+            tc = (time.perf_counter() - tc) / 5
+            td = time.perf_counter()
+            for _ in range(5):
+                cz.decompress_host(hp_out, shape, dtype, maxbits, out=hp_back)
+            td = (time.perf_counter() - td) / 5
+            host_path = {"compress_GBps": round(n_in / tc / 1e9, 2), "decompress_GBps": round(n_in / td / 1e9, 2),
+                         "roundtrip_GBps": round(n_in / (tc + td) / 1e9, 2),
+                         "note": "pinned host buffers, PCIe-inclusive (cuzfp_hip_compress_host/decompress_host)"}
+        cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(a, maxbits)
+        result = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32" if args.dtype == "float32" else "f64",
+            "data": f"synthetic ({'testzfp polynomial field' if args.field == 'polynomial' else 'splitmix64 uniform [-1,1)'})",
+            "config": {"workload": f"3d_{args.dtype}_{n}^3_rate{args.rate:g}", "shape_per_gpu": list(shape),
+                       "global_shape": list(gshape), "maxbits": maxbits, "rate": args.rate,
+                       "parallelism": f"z-slab x{world}", "stream_bytes_per_gpu": s_bytes},
+            "pct_hbm_peak": round(100.0 * value / world * (enc_bytes + dec_bytes) / n_in / HBM_PEAK_GBS, 2),
+            "gpu_ms_per_step": round(gpu_ms_per_step, 4),
+            "encode_ms": round(enc_ms, 4),
+            "decode_ms": round(dec_ms, 4),
+            "encode_GBps_input": round(n_in / (enc_ms * 1e-3) / 1e9, 1),
+            "decode_GBps_input": round(n_in / (dec_ms * 1e-3) / 1e9, 1),
+            "roofline": {"bound": "hbm", "kernel": f"zfp_{dominant}", "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "algorithmic_bytes_per_launch": dom_bytes},
+            "cpu_baseline": cpu,
+            "host_path": host_path,
+            "allgather": allgather,
+            "max_abs_err": max_err,
+            "parity": parity,
+        }
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return result
+
+
+if __name__ == "__main__":
+    main()

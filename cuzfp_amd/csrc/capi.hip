@@ -311,15 +311,11 @@ size_t cuzfp_hip_stream_bytes(int type, unsigned nx, unsigned ny, unsigned nz, u
 }
 
 size_t cuzfp_hip_maximum_size(int type, unsigned nx, unsigned ny, unsigned nz, unsigned maxbits) {
-  // zfp_structs.h:237-266 with the reference's header allowance of 148 bits
+  // zfp_structs.h:237-266 in fixed-rate mode: minbits == maxbits, so every
+  // block is exactly maxbits bits; plus the reference's 148-bit header allowance
   Problem p;
   if (make_problem(type, nx, ny, nz, 0, 0, 0, maxbits, &p) != CUZFP_SUCCESS) return 0;
-  const unsigned values = 1u << (2 * p.dims);
-  const unsigned prec = (type == CUZFP_TYPE_FLOAT || type == CUZFP_TYPE_INT32) ? 32 : 64;
-  unsigned mb = 1 + (type == CUZFP_TYPE_FLOAT ? 8 : type == CUZFP_TYPE_DOUBLE ? 11 : 0);
-  mb += values - 1 + values * prec;
-  mb = std::min(mb, maxbits);
-  return ((148 + (size_t)p.g.nblocks * mb + 63) & ~(size_t)63) / 8;
+  return ((148 + (size_t)p.g.nblocks * maxbits + 63) & ~(size_t)63) / 8;
 }
 
 int cuzfp_hip_encode(const void* d_data, int type, unsigned nx, unsigned ny, unsigned nz,

@@ -110,12 +110,19 @@ class Restatement(_Codec):
             f = getattr(lib, name)
             f.restype = _i
             f.argtypes = [_i, _u, _u, _u, _i, _i, _i, _u, _vp, _sz, _vp]
+        lib.oracle_jenkins_hash.restype = ctypes.c_uint32
+        lib.oracle_jenkins_hash.argtypes = [_vp, _sz]
         lib.oracle_rate_to_maxbits.restype = _u
         lib.oracle_rate_to_maxbits.argtypes = [ctypes.c_double, _i, _u, _i]
         super().__init__(lib, "restatement")
 
     def rate_to_maxbits(self, rate: float, dtype, dims: int, wra: bool = False) -> int:
         return self.lib.oracle_rate_to_maxbits(rate, TYPE_CODES[np.dtype(dtype)], dims, int(wra))
+
+    def jenkins_hash(self, a: np.ndarray) -> int:
+        """testzfp's array checksum (testzfp.cpp:74-89)."""
+        a = np.ascontiguousarray(a)
+        return int(self.lib.oracle_jenkins_hash(a.ctypes.data, a.nbytes))
 
     def _compress(self, t, nx, ny, nz, st, maxbits, a, out, cap):
         f = self.lib.oracle_compress if t >= 3 else self.lib.oracle_compress_int

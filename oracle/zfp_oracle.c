@@ -534,3 +534,19 @@ int oracle_decompress_int(int type, unsigned nx, unsigned ny, unsigned nz,
   }
   return 1;
 }
+
+/* Jenkins one-at-a-time hash, the array checksum of zfp-0.5.0/tests/testzfp.cpp:74-89 */
+uint32_t oracle_jenkins_hash(const void* p, size_t n)
+{
+  const unsigned char* q = (const unsigned char*)p;
+  uint32_t h = 0;
+  for (; n; q++, n--) {
+    h += *q;
+    h += h << 10;
+    h ^= h >> 6;
+  }
+  h += h << 3;
+  h ^= h >> 11;
+  h += h << 15;
+  return h;
+}

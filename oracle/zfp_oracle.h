@@ -56,6 +56,9 @@ int oracle_decompress_int(int type, unsigned nx, unsigned ny, unsigned nz,
                           int sx, int sy, int sz, unsigned maxbits,
                           const void* stream, size_t stream_bytes, void* data);
 
+/* Jenkins one-at-a-time hash (zfp-0.5.0/tests/testzfp.cpp:74-89). */
+uint32_t oracle_jenkins_hash(const void* p, size_t n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,106 @@
+"""The C-ABI boundary (CPU-only: no kernel launches).
+
+* libcuzfp_hip.so loads and exports every function include/cuzfp_hip.h declares;
+* libcuZFP.so exports the reference's C++ entry points cuZFP::compress /
+  cuZFP::decompress (src/cuZFP/cuZFP.h:9-10);
+* the host-only helpers agree with the oracle / reference formulas;
+* argument errors come back as status codes before any device work.
+"""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import cuzfp_amd as cz
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "cuzfp_hip.h")
+
+
+@pytest.fixture(scope="module")
+def libs():
+    from cuzfp_amd.build import build
+    return build()
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(cuzfp_hip_\w+)\s*\(", text)))
+
+
+def exported(path):
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if line.strip()}
+
+
+def test_header_symbols_exported(libs):
+    syms = exported(libs["hip"])
+    names = declared_functions()
+    assert len(names) >= 10
+    missing = [n for n in names if n not in syms]
+    assert not missing, missing
+
+
+def test_cpp_dropin_symbols(libs):
+    out = subprocess.run(["nm", "-DC", "--defined-only", libs["cpp"]], capture_output=True, text=True).stdout
+    assert "cuZFP::compress(cuZFP::zfp_stream*, cuZFP::zfp_field*)" in out
+    assert "cuZFP::decompress(cuZFP::zfp_stream*, cuZFP::zfp_field*)" in out
+
+
+def test_library_loads(libs):
+    lib = cz.library()
+    assert lib.cuzfp_hip_abi_version() == 1
+    assert lib.cuzfp_hip_status_string(0) == b"success"
+    assert lib.cuzfp_hip_status_string(3) == b"stream buffer too small"
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_rate_to_maxbits_matches_zfp(libs, restatement, dtype):
+    for dims in (1, 2, 3):
+        for rate in (0.25, 1, 1.5, 2, 7.9, 8, 16, 31, 64):
+            for wra in (False, True):
+                assert cz.rate_to_maxbits(rate, dtype, dims, wra) == restatement.rate_to_maxbits(rate, dtype, dims, wra)
+
+
+def test_stream_bytes(libs, restatement):
+    for shape in [(1,), (5,), (1 << 20,), (3, 7), (8192, 8192), (1, 1, 1), (13, 17, 19), (256, 256, 256)]:
+        for mb in (9, 32, 100, 512, 1024):
+            assert cz.stream_bytes(shape, np.float32, mb) == restatement.stream_bytes(shape, mb)
+
+
+def test_maximum_size(libs, reference):
+    for shape in [(100,), (64, 64), (16, 8, 4), (13, 17, 19)]:
+        for dt, mb in ((np.float32, 512), (np.float64, 1024), (np.float32, 4171)):
+            nx, ny, nz = (tuple(shape[::-1]) + (0, 0))[:3]
+            want = reference.lib.ref_maximum_size
+            want.restype = ctypes.c_size_t
+            want.argtypes = [ctypes.c_int] + [ctypes.c_uint] * 4
+            got = cz.maximum_size(shape, dt, mb)
+            assert got >= cz.stream_bytes(shape, dt, mb)
+            # zfp_stream_maximum_size with minbits == maxbits (fixed rate)
+            assert got == want(3 if dt == np.float32 else 4, nx, ny, nz, mb)
+
+
+def test_argument_errors(libs):
+    lib = cz.library()
+    got = ctypes.c_size_t(0)
+    buf = ctypes.c_void_p(0x1000)  # never dereferenced: rejected before any launch
+    # unsupported type
+    assert lib.cuzfp_hip_encode(buf, 9, 16, 16, 16, 0, 0, 0, 512, buf, 1 << 20, ctypes.byref(got), None) == 2
+    # nz without ny, nx == 0
+    assert lib.cuzfp_hip_encode(buf, 3, 16, 0, 16, 0, 0, 0, 512, buf, 1 << 20, ctypes.byref(got), None) == 1
+    assert lib.cuzfp_hip_encode(buf, 3, 0, 0, 0, 0, 0, 0, 512, buf, 1 << 20, ctypes.byref(got), None) == 1
+    # maxbits below the exponent header
+    assert lib.cuzfp_hip_encode(buf, 3, 16, 16, 16, 0, 0, 0, 8, buf, 1 << 20, ctypes.byref(got), None) == 1
+    assert lib.cuzfp_hip_encode(buf, 4, 16, 16, 16, 0, 0, 0, 11, buf, 1 << 20, ctypes.byref(got), None) == 1
+    # stream too small
+    assert lib.cuzfp_hip_encode(buf, 3, 16, 16, 16, 0, 0, 0, 512, buf, 100, ctypes.byref(got), None) == 3
+    assert lib.cuzfp_hip_decode(buf, 100, 3, 16, 16, 16, 0, 0, 0, 512, buf, None) == 3
+    # null pointers
+    assert lib.cuzfp_hip_encode(None, 3, 16, 16, 16, 0, 0, 0, 512, buf, 1 << 20, ctypes.byref(got), None) == 1
+    assert lib.cuzfp_hip_compress_host(None, 3, 16, 16, 16, 512, buf, 1 << 20, ctypes.byref(got), 2) == 1
+    with pytest.raises(cz.CodecError):
+        cz.stream_bytes((16, 16, 16), np.float32, 3)

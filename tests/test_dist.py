@@ -1,0 +1,74 @@
+"""Multi-process sharding (CPU, gloo, world_size 2).
+
+Each rank compresses its z-slab (cuzfp_amd.dist.slab_extent) -- here with the
+CPU oracle standing in for the kernel, since this container has no GPU -- and
+one all-gather (cuzfp_amd.dist.allgather_stream) must reproduce, on every rank,
+the single-process stream of the whole array bit-for-bit.
+The GPU leg of the same path runs in bench.py over RCCL.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, shape, maxbits, q):
+    import torch
+    import torch.distributed as dist
+    import oracle
+    from cuzfp_amd import dist as zd
+    from cuzfp_amd.datagen import splitmix_uniform
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        a = splitmix_uniform(shape, np.float32, seed=3)
+        z0, z1 = zd.slab_extent(shape[0], world, rank)
+        local = np.ascontiguousarray(a[z0:z1])
+        words = oracle.restatement.compress(local, maxbits).view(np.int64)
+        assert words.size == zd.segment_words(shape, world, maxbits)
+        full = zd.allgather_stream(torch.from_numpy(words.copy()))
+        q.put((rank, full.numpy().view(np.uint64).copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("shape,maxbits", [((32, 12, 20), 512), ((16, 16), 32), ((64,), 128)])
+def test_allgather_rebuilds_stream(shape, maxbits, restatement):
+    import multiprocessing as mp
+    from cuzfp_amd import dist as zd
+    from cuzfp_amd.datagen import splitmix_uniform
+    world = 2
+    assert zd.uniform_shard_ok(shape, world, maxbits)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, shape, maxbits, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = restatement.compress(splitmix_uniform(shape, np.float32, seed=3), maxbits)
+    for r in range(world):
+        assert np.array_equal(results[r], want)
+
+
+def test_slab_extent_covers():
+    from cuzfp_amd import dist as zd
+    for n in (1, 4, 5, 17, 64, 1024):
+        for world in (1, 2, 3, 8):
+            spans = [zd.slab_extent(n, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            for (a0, a1), (b0, b1) in zip(spans, spans[1:]):
+                assert a1 == b0 and (a0 % 4 == 0 or a0 == n)

@@ -72,3 +72,175 @@ def test_fuzz_vs_oracle(dims, dtype, kind, cuda, restatement):
         assert np.array_equal(words, ref), (shape, mb)
         dref = restatement.decompress(ref, shape, dtype, mb)
         assert np.array_equal(y.view(np.uint8), dref.view(np.uint8)), (shape, mb)
+
+
+# --------------------------------------------------------------------------
+# committed golden fixtures (reference zfp 0.5.0 output, tests/golden/)
+
+import hashlib
+import json
+import os
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def _golden():
+    with open(os.path.join(GOLDEN, "golden.json")) as f:
+        return json.load(f)["cases"]
+
+
+def test_golden_fields_and_ramps(cuda):
+    from cuzfp_amd.datagen import ramp
+    g = _golden()
+    fields = dict(np.load(os.path.join(GOLDEN, "fields.npz")))
+    streams = {k.replace("__", "/"): v for k, v in np.load(os.path.join(GOLDEN, "streams.npz")).items()}
+    for name, s in streams.items():
+        rec = g[name]
+        a = fields[name.split("/")[1]] if name.startswith("fields/") else ramp(tuple(rec["shape"]), np.dtype(rec["dtype"]))
+        words, y = _gpu_roundtrip(a, rec["maxbits"], cuda)
+        assert np.array_equal(words, s), name
+        # decoding the reference stream reproduces the reference's decoded array
+        import torch
+        dec = cz.decode(torch.from_numpy(s.view(np.int64).copy()).to(cuda), a.shape,
+                        torch.from_numpy(a).dtype, rec["maxbits"]).cpu().numpy()
+        assert _sha(dec) == rec["decoded_sha256"], name
+
+
+def test_golden_fuzz(cuda):
+    from cuzfp_amd.datagen import splitmix_uniform
+    for name, rec in _golden().items():
+        if not name.startswith("fuzz/"):
+            continue
+        dt = np.dtype(rec["dtype"])
+        a = (splitmix_uniform(tuple(rec["shape"]), dt, rec["seed"]) * (10.0 ** rec["scale_exp10"])).astype(dt)
+        words, y = _gpu_roundtrip(a, rec["maxbits"], cuda)
+        assert _sha(words) == rec["stream_sha256"], name
+        assert _sha(y) == rec["decoded_sha256"], name
+
+
+@pytest.mark.parametrize("name", ["baseline/3d_f32_256_r8", "baseline/3d_f64_256_r16",
+                                  "baseline/2d_f32_8192_r2", "baseline/1d_f32_1M_r8"])
+@pytest.mark.parametrize("gen", ["polynomial", "splitmix"])
+def test_golden_baseline_configs(cuda, name, gen):
+    """BASELINE.json's full-size configurations: stream and decoded array hash-equal
+    to the reference's own zfp 0.5.0 output."""
+    from cuzfp_amd.datagen import polynomial_field, splitmix_uniform
+    rec = _golden()[f"{name}/{gen}"]
+    dt = np.dtype(rec["dtype"])
+    shape = tuple(rec["shape"])
+    a = polynomial_field(shape, dt) if gen == "polynomial" else splitmix_uniform(shape, dt, rec["seed"])
+    words, y = _gpu_roundtrip(a, rec["maxbits"], cuda)
+    assert words.nbytes == rec["bytes"]
+    assert _sha(words) == rec["stream_sha256"]
+    assert _sha(y) == rec["decoded_sha256"]
+
+
+# --------------------------------------------------------------------------
+# integer fields, strides, extremes, host pipeline, sizes
+
+
+@pytest.mark.parametrize("dims", [1, 2, 3])
+@pytest.mark.parametrize("dtype", [np.int32, np.int64])
+def test_int_fields(cuda, restatement, dims, dtype):
+    rng = np.random.default_rng(dims * 3 + (dtype == np.int64))
+    for trial in range(6):
+        hi = {1: 300, 2: 60, 3: 20}[dims]
+        shape = tuple(int(rng.integers(1, hi)) for _ in range(dims))
+        lim = 2 ** (20 if trial % 2 else 30)
+        a = rng.integers(-lim, lim, size=shape).astype(dtype)
+        mb = int(rng.integers(2, 3000))
+        words, y = _gpu_roundtrip(a, mb, cuda)
+        ref = restatement.compress(a, mb)
+        assert np.array_equal(words, ref)
+        assert np.array_equal(y, restatement.decompress(ref, shape, dtype, mb))
+
+
+def test_strided_views(cuda, restatement):
+    """Non-contiguous device views (positive and negative strides) vs the
+    restatement with the same strides (zfp honours sx/sy/sz; cuZFP ignored them)."""
+    import ctypes
+    import torch
+    rng = np.random.default_rng(21)
+    base = rng.standard_normal((16, 12, 26)).astype(np.float32)
+    tb = torch.from_numpy(base).to(cuda)
+    for sl in [(slice(None, None, 2), slice(None), slice(1, 19)),
+               (slice(None), slice(None, None, -1), slice(None, None, -2)),
+               (slice(3, 14), slice(2, 11), slice(None, None, 3))]:
+        view_t = tb[sl]
+        view_n = base[sl]
+        nz, ny, nx = view_n.shape
+        st = tuple(s // 4 for s in view_n.strides[::-1])
+        mb = 384
+        cap = restatement.stream_bytes(view_n.shape, mb) + 64
+        ref = np.zeros(cap // 8, np.uint64)
+        n = restatement.lib.oracle_compress(3, nx, ny, nz, st[0], st[1], st[2], mb,
+                                            view_n.__array_interface__["data"][0], ref.ctypes.data, cap)
+        words = cz.encode(view_t, mb)
+        torch.cuda.synchronize()
+        assert np.array_equal(words.cpu().numpy().view(np.uint64), ref[: n // 8])
+        # decode into a strided destination, leaving the gaps untouched
+        dst = torch.full_like(tb, -7.0)
+        cz.decode(words, view_t.shape, view_t.dtype, mb, out=dst[sl])
+        torch.cuda.synchronize()
+        got = dst.cpu().numpy()
+        want = restatement.decompress(ref[: n // 8], view_n.shape, np.float32, mb)
+        assert np.array_equal(got[sl], want)
+        mask = np.ones(base.shape, bool)
+        mask[sl] = False
+        assert np.all(got[mask] == -7.0)
+    del ctypes
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_extreme_blocks(cuda, restatement, dtype):
+    rng = np.random.default_rng(9)
+    scales = [1e-30, 1e-38, 1e-44, 3e38] if dtype == np.float32 else [1e-300, 1e-310, 1e-320, 1e308]
+    for sc in scales:
+        a = (rng.standard_normal((12, 8, 8)) * sc).astype(dtype)
+        a.flat[::5] = 0
+        a[0, 0, 0] = np.inf if sc > 1 else a[0, 0, 0]
+        for mb in (restatement.rate_to_maxbits(1, dtype, 3), 512, 1000, 4171):
+            words, y = _gpu_roundtrip(a, mb, cuda)
+            ref = restatement.compress(a, mb)
+            assert np.array_equal(words, ref)
+            assert np.array_equal(y.view(np.uint8), restatement.decompress(ref, a.shape, dtype, mb).view(np.uint8))
+
+
+@pytest.mark.parametrize("shape", [(1,), (3,), (5, 7), (1, 1, 1), (2, 3, 5), (64, 64, 64), (4, 4, 4 * 4097)])
+def test_edge_sizes(cuda, restatement, shape):
+    """Empty-ish, ragged and multi-wave arrays (a wave = 64 blocks)."""
+    from cuzfp_amd.datagen import splitmix_uniform
+    for mb in (9, 32, 77, 512):
+        a = splitmix_uniform(shape, np.float32, seed=len(shape) + mb)
+        words, y = _gpu_roundtrip(a, mb, cuda)
+        ref = restatement.compress(a, mb)
+        assert np.array_equal(words, ref), (shape, mb)
+        assert np.array_equal(y, restatement.decompress(ref, shape, np.float32, mb))
+
+
+@pytest.mark.parametrize("shape,dtype,rate", [((96, 80, 72), np.float32, 8), ((40, 36, 20), np.float64, 16),
+                                              ((1000, 700), np.float32, 2), ((300001,), np.float32, 8),
+                                              ((33, 34, 35), np.float32, 5.5)])
+@pytest.mark.parametrize("pinned", [False, True])
+def test_host_pipeline(cuda, restatement, shape, dtype, rate, pinned):
+    """cuzfp_hip_compress_host / decompress_host (pinned chunked pipeline) ==
+    the device path == the oracle, from pageable and from pinned buffers."""
+    import torch
+    from cuzfp_amd.datagen import splitmix_uniform
+    a = splitmix_uniform(shape, dtype, seed=5)
+    mb = cz.rate_to_maxbits(rate, dtype, len(shape))
+    out = None
+    if pinned:
+        host = torch.from_numpy(a).pin_memory()
+        a = host.numpy()
+        out = torch.empty(cz.stream_bytes(shape, dtype, mb) // 8, dtype=torch.int64).pin_memory().numpy().view(np.uint64)
+    for nstreams in (1, 3):
+        s = cz.compress_host(a, mb, nstreams=nstreams, out=out)
+        ref = restatement.compress(a, mb)
+        assert np.array_equal(s, ref)
+        y = cz.decompress_host(s, shape, dtype, mb, nstreams=nstreams)
+        assert np.array_equal(y, restatement.decompress(ref, shape, dtype, mb))

@@ -1,0 +1,51 @@
+#!/bin/bash
+# tools/gpu_session.sh -- one GPU-box session: parity tests, bench, rocprofv3.
+# Every GPU step has its own time limit; a crash / abort / timeout (exit codes
+# other than 0 and pytest's 1 = "tests failed") ends the session at once.
+# Usage (from the repo root on the box):  bash tools/gpu_session.sh [tag] [steps...]
+set -u
+TAG=${1:-run}
+shift || true
+STEPS=${*:-"pytest bench prof"}
+OUT=${GRAFT_REPO_ROOT:-$PWD}/gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+ok_or_stop() {  # $1 = rc, $2 = step name
+  local rc=$1
+  echo "[$2] exit $rc"
+  if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then echo "[$2] abnormal exit: stopping"; exit "$rc"; fi
+}
+for s in $STEPS; do
+  case $s in
+    pytest)
+      timeout -k 10 1200 python -m pytest tests -m gpu -x -q -p no:cacheprovider > "$OUT/pytest_gpu_$TAG.log" 2>&1
+      ok_or_stop $? pytest; tail -5 "$OUT/pytest_gpu_$TAG.log" ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke_$TAG.log" 2>&1
+      ok_or_stop $? smoke; tail -2 "$OUT/smoke_$TAG.log" ;;
+    bench)
+      timeout -k 10 600 python bench.py > "$OUT/bench_$TAG.json" 2> "$OUT/bench_$TAG.err"
+      ok_or_stop $? bench; cat "$OUT/bench_$TAG.json" ;;
+    benchsplit)
+      timeout -k 10 300 python bench.py --field splitmix --no-cpu-baseline --no-host-path > "$OUT/bench_splitmix_$TAG.json" 2>&1
+      ok_or_stop $? benchsplit; cat "$OUT/bench_splitmix_$TAG.json" ;;
+    bench64)
+      timeout -k 10 300 python bench.py --dtype float64 --rate 16 --no-cpu-baseline --no-host-path > "$OUT/bench_f64_$TAG.json" 2>&1
+      ok_or_stop $? bench64; cat "$OUT/bench_f64_$TAG.json" ;;
+    prof)
+      rm -rf "$OUT/prof_$TAG"
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run -- \
+        python bench.py --steps 20 --no-cpu-baseline --no-host-path > "$OUT/prof_bench_$TAG.json" 2>&1
+      ok_or_stop $? prof
+      find "$OUT/prof_$TAG" -name "*kernel_stats.csv" -exec head -8 {} \; ;;
+    pmc)
+      rm -rf "$OUT/pmc_$TAG"
+      timeout -k 10 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/pmc_$TAG/fetch" -o run -- \
+        python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-host-path > /dev/null 2>&1
+      ok_or_stop $? pmc_fetch
+      timeout -k 10 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/pmc_$TAG/write" -o run -- \
+        python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-host-path > /dev/null 2>&1
+      ok_or_stop $? pmc_write ;;
+    *) echo "unknown step $s" ;;
+  esac
+done
