@@ -48,7 +48,8 @@ _lib = None
 
 
 def library_path() -> str:
-    return os.path.join(LIB_DIR, "libcuzfp_hip.so")
+    """The in-tree build; CUZFP_HIP_LIB overrides it (A/B runs of kernel variants)."""
+    return os.environ.get("CUZFP_HIP_LIB") or os.path.join(LIB_DIR, "libcuzfp_hip.so")
 
 
 def library() -> ctypes.CDLL:

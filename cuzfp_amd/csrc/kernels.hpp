@@ -29,52 +29,76 @@ namespace cuzfp {
 // ---------------------------------------------------------------------------
 // LDS bit writers / reader (one lane, one block)
 
-// maxbits % 64 == 0: the lane owns whole words [lane*W, lane*W + W).
+// maxbits % 64 == 0: the lane owns whole words [lane*W, lane*W + W).  Full
+// 64-bit words are flushed to LDS; once W words are out the block is full, so
+// bits the coder produced past maxbits stay in `acc` and are dropped.
 struct LdsWordWriter {
   uint64_t* p;
   uint32_t words, w, cnt;
   uint64_t acc;
+  __device__ __forceinline__ bool full() const { return w >= words; }
   __device__ __forceinline__ void put(uint64_t v, unsigned n) {
     acc |= v << cnt;
-    if (cnt + n >= 64) {
+    const unsigned c = cnt + n;
+    if (c >= 64) {
       p[w++] = acc;
-      acc = cnt ? v >> (64 - cnt) : 0;
-      cnt = cnt + n - 64;
+      acc = (v >> 1) >> (63 - cnt);  // the bits of v that did not fit (0 if cnt == 0)
+      cnt = c - 64;
     } else {
-      cnt += n;
+      cnt = c;
+    }
+  }
+  __device__ __forceinline__ void zero_bit() {
+    if (++cnt == 64) {
+      p[w++] = acc;
+      acc = 0;
+      cnt = 0;
     }
   }
   __device__ __forceinline__ void finish() {
-    if (cnt) p[w++] = acc;
-    while (w < words) p[w++] = 0;
+    if (w < words) {
+      p[w++] = acc;
+      while (w < words) p[w++] = 0;
+    }
   }
 };
 
-// general maxbits: the lane's bits start at lane*maxbits; full 64-bit chunks
-// are OR-ed into the (zeroed) LDS image with ds_or_b64, since the first and
-// last words of a lane's range are shared with its neighbours.
+// general maxbits: the lane's bits are [pos0, end) of the wave's segment;
+// 64-bit chunks are OR-ed into the (zeroed) LDS image with ds_or_b64, since
+// the first and last words of a lane's range are shared with its neighbours.
 struct LdsBitWriter {
   uint64_t* lds;
-  uint32_t start, cnt;
+  uint32_t pos, end, cnt;  // pos: stream offset of acc's bit 0
   uint64_t acc;
+  __device__ __forceinline__ bool full() const { return pos + cnt >= end; }
   __device__ __forceinline__ void emit(uint64_t v) {
-    const uint32_t w = start >> 6, sh = start & 63;
+    const uint32_t room = end - pos;
+    if (room < 64) v &= lowmask(room);
+    const uint32_t w = pos >> 6, sh = pos & 63;
     atomicOr((unsigned long long*)&lds[w], (unsigned long long)(v << sh));
     if (sh) atomicOr((unsigned long long*)&lds[w + 1], (unsigned long long)(v >> (64 - sh)));
-    start += 64;
+    pos += 64;
   }
   __device__ __forceinline__ void put(uint64_t v, unsigned n) {
     acc |= v << cnt;
-    if (cnt + n >= 64) {
+    const unsigned c = cnt + n;
+    if (c >= 64) {
       emit(acc);
-      acc = cnt ? v >> (64 - cnt) : 0;
-      cnt = cnt + n - 64;
+      acc = (v >> 1) >> (63 - cnt);
+      cnt = c - 64;
     } else {
-      cnt += n;
+      cnt = c;
+    }
+  }
+  __device__ __forceinline__ void zero_bit() {
+    if (++cnt == 64) {
+      emit(acc);
+      acc = 0;
+      cnt = 0;
     }
   }
   __device__ __forceinline__ void finish() {
-    if (cnt) emit(acc);
+    if (cnt && pos < end) emit(acc);
   }
 };
 
@@ -216,7 +240,7 @@ __device__ __forceinline__ void scatter(Scalar* __restrict__ data, const Geometr
 // Kernels
 
 template <typename Scalar, int DIMS, bool FAST, bool ALIGNED>
-__global__ __launch_bounds__(kLanes) void zfp_encode(const Scalar* __restrict__ data, Geometry g,
+__global__ __launch_bounds__(kLanes, 4) void zfp_encode(const Scalar* __restrict__ data, Geometry g,
                                                      uint64_t* __restrict__ stream) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
   constexpr int N = 1 << (2 * DIMS);
@@ -235,7 +259,7 @@ __global__ __launch_bounds__(kLanes) void zfp_encode(const Scalar* __restrict__ 
       LdsWordWriter wr{lds + lane * W, W, 0, 0, 0};
       encode_block<Scalar, DIMS>(f, g.maxbits, wr);
     } else {
-      LdsBitWriter wr{lds, lane * g.maxbits, 0, 0};
+      LdsBitWriter wr{lds, lane * g.maxbits, (lane + 1) * g.maxbits, 0, 0};
       encode_block<Scalar, DIMS>(f, g.maxbits, wr);
     }
   }
@@ -254,7 +278,7 @@ __global__ __launch_bounds__(kLanes) void zfp_encode(const Scalar* __restrict__ 
 }
 
 template <typename Scalar, int DIMS, bool FAST>
-__global__ __launch_bounds__(kLanes) void zfp_decode(const uint64_t* __restrict__ stream,
+__global__ __launch_bounds__(kLanes, 4) void zfp_decode(const uint64_t* __restrict__ stream,
                                                      Geometry g, Scalar* __restrict__ data) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
   constexpr int N = 1 << (2 * DIMS);

@@ -2,7 +2,7 @@
 //
 // This header is the arithmetic of the MI355X codec: everything a single lane
 // does to turn one 4^d block of scalars into `maxbits` stream bits and back.
-// The HIP kernels (codec_kernels.hip) wrap it with coalesced HBM gathers and an
+// The HIP kernels (kernels.hpp) wrap it with coalesced HBM gathers and an
 // LDS-staged bitstream; tests/emulate.cpp runs the very same functions on the
 // host so the per-lane algorithm is checked against the CPU oracle without a GPU.
 //
@@ -271,6 +271,32 @@ template <typename UInt, int DIMS> struct planes {
     for (int h = 0; h < H; h++)
 #pragma unroll
       for (int g = 0; g < G; g++) transpose_tiles<R>(&w[h][g * R]);
+    pin();
+  }
+
+  // Materialise every plane word here: without this the compiler sinks the
+  // transpose stages into the plane loop and keeps pre- and post-transpose
+  // copies alive at once, which costs registers (occupancy).
+  // For 64 coefficients each plane is pinned as one 64-bit register pair, the
+  // operand form of the plane coder's 64-bit shifts.
+  ZFP_HD void pin() {
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+    for (int h = 0; h < H; h++) {
+      if constexpr (N == 64) {
+#pragma unroll
+        for (int c = 0; c < 32; c++) {
+          uint64_t v = (uint64_t)w[h][c] | ((uint64_t)w[h][32 + c] << 32);
+          asm volatile("" : "+v"(v));
+          w[h][c] = (uint32_t)v;
+          w[h][32 + c] = (uint32_t)(v >> 32);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < N; i++) asm volatile("" : "+v"(w[h][i]));
+      }
+    }
+#endif
   }
 
   ZFP_HD void store(UInt* u) {
@@ -318,94 +344,137 @@ template <typename UInt, int DIMS> struct planes {
 // most significant first: the first n bits verbatim (coefficients already
 // significant), then group tests: "1" + the bits up to and including the next
 // one bit (the one at position N-1 is implied), until a "0" test or the end of
-// the plane.  Each group is emitted with one writer call; a call that would
-// overrun the budget is cut to the remaining bits, which makes the output
-// exactly the reference's prefix.
+// the plane.  Each group is emitted with one writer call.
+
+// Plane word type: 64 coefficients need 64 bits, 16 or 4 fit in 32.
+template <int DIMS> struct plane_word { typedef uint32_t type; };
+template <> struct plane_word<3> { typedef uint64_t type; };
+
+ZFP_HD unsigned ctz(uint32_t x) { return (unsigned)__builtin_ctz(x); }  // x != 0
+ZFP_HD unsigned ctz(uint64_t x) { return (unsigned)__builtin_ctzll(x); }
+
+// count of trailing zeros, 64 for x == 0 (v_ffbl_b32 returns ~0 for a zero word)
+ZFP_HD unsigned ctz64_or_64(uint64_t x) {
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  const unsigned zl = lo ? (unsigned)__builtin_ctz(lo) : 64u;
+  const unsigned zh = hi ? 32u + (unsigned)__builtin_ctz(hi) : 64u;
+  return zl < zh ? zl : zh;
+}
 
 // The plane loop is unrolled by template recursion so that plane K is a
 // compile-time register index (a runtime-indexed plane array would live in
-// scratch memory).  A lane that runs out of budget returns; the wave walks on
-// only while some lane still has bits left.
+// scratch memory).  A lane whose block is full returns; the wave walks on only
+// while some lane still has bits left.
+//
+// Encoder plane step.  With n coefficients already significant the plane's code
+// is: its first n bits verbatim, then for every further one bit at position p
+// a group "1" + the zeros before p + that one (implied, so omitted, when
+// p = N-1), then a closing "0" group test if positions remain.  Positions are
+// absolute (r keeps the not-yet-coded ones), so every group costs one ctz, one
+// put and one r &= r - 1.  The writer is never asked to clip: it reports
+// full() once the block's maxbits are written and the loop stops there, so the
+// stream is exactly the reference's budget-truncated prefix.
 template <int K, typename UInt, int DIMS, typename Writer>
-ZFP_HD void encode_planes_from(const planes<UInt, DIMS>& P, unsigned& bits, unsigned& n, int kmin,
-                               Writer& wr) {
+ZFP_HD void encode_planes_from(const planes<UInt, DIMS>& P, unsigned& n, int kmin, Writer& wr) {
   if constexpr (K >= 0) {
+    typedef typename plane_word<DIMS>::type PW;
     constexpr unsigned N = 1u << (2 * DIMS);
-    if (!bits || K < kmin) return;
-    const uint64_t x = P.get(K);
-    // verbatim part: the n coefficients already known to be significant
-    const unsigned m = umin(n, bits);
-    wr.put(x & lowmask(m), m);
-    bits -= m;
-    uint64_t r = n < N ? x >> n : 0;
-    while (n < N && bits) {
-      if (!r) {  // group test fails: plane done
-        wr.put(0, 1);
-        bits--;
-        break;
+    if (wr.full() || K < kmin) return;
+    const PW x = (PW)P.get(K);
+    // verbatim part
+    if (n) wr.put(x & (PW)lowmask(n), n);
+    // new ones, in the frame of the first not-yet-significant coefficient
+    const PW r = n < N ? (PW)(x >> n) : (PW)0;
+    if (!r) {
+      if (n < N && !wr.full()) wr.zero_bit();  // group test "0"
+    } else if (!wr.full()) {
+      // With t new ones at relative positions p_0 < ... < p_{t-1} the group
+      // code is  1 (z_0 zeros) 1 1 (z_1 zeros) 1 1 ... (z_{t-1} zeros) 1 0,
+      // i.e. "1" followed by the segment up to p_{t-1} with every one doubled,
+      // the last one's partner being the closing "0" -- or, when the last one
+      // sits at position N-1, both its bit and the closing test omitted.  The
+      // j-th one therefore lands at bit p_j + j + 1 (and its partner at + 2):
+      // F collects those positions with one shift per one, no branches on the
+      // stream.
+      const unsigned pt = (unsigned)(8 * sizeof(PW) - 1) - (unsigned)(sizeof(PW) == 8 ? __builtin_clzll((uint64_t)r) : __builtin_clz((uint32_t)r));
+      const unsigned t = (unsigned)(sizeof(PW) == 8 ? __builtin_popcountll((uint64_t)r) : __builtin_popcount((uint32_t)r));
+      const unsigned qmax = pt + t - 1;  // F position of the last one
+      const bool last_n = pt + n == N - 1;
+      if (qmax <= 61) {
+        uint64_t F = 0;
+        PW rr = r;
+        unsigned j = 0;
+        while (rr) {
+          const PW low = rr & (PW)(0 - rr);
+          F |= (uint64_t)low << j;
+          rr ^= low;
+          j++;
+        }
+        const unsigned L = qmax + (last_n ? 1u : 3u);
+        const uint64_t G = (1ull | (F << 1) | (F << 2)) & lowmask(last_n ? L : L - 1);
+        wr.put(G, L);
+        n += pt + 1;
+      } else {
+        // dense plane (many ones early in a wide block): one put per group
+        PW rest = r;
+        unsigned base = n;
+        while (rest && !wr.full()) {
+          const unsigned p = ctz(rest);
+          const bool last = base + p == N - 1;
+          const unsigned z = p - (n - base);
+          wr.put(last ? 1ull : (1ull | (2ull << z)), z + (last ? 1u : 2u));
+          n = base + p + 1;
+          rest &= rest - 1;
+        }
+        if (n < N && !wr.full()) wr.zero_bit();
       }
-      const unsigned z = ctz64(r);
-      const unsigned p = n + z;
-      const bool last = p == N - 1;
-      unsigned len = z + (last ? 1u : 2u);
-      uint64_t code = last ? 1ull : (1ull | (2ull << z));
-      if (len > bits) {
-        len = bits;
-        code &= lowmask(len);
-      }
-      wr.put(code, len);
-      bits -= len;
-      n = p + 1;
-      r = (z < 63) ? r >> (z + 1) : 0;
     }
-    encode_planes_from<K - 1, UInt, DIMS>(P, bits, n, kmin, wr);
+    encode_planes_from<K - 1, UInt, DIMS>(P, n, kmin, wr);
   }
 }
 
 template <typename UInt, int DIMS, typename Writer>
-ZFP_HD void encode_planes(const planes<UInt, DIMS>& P, unsigned budget, unsigned maxprec,
-                          Writer& wr) {
+ZFP_HD void encode_planes(const planes<UInt, DIMS>& P, unsigned maxprec, Writer& wr) {
   constexpr int PREC = (int)sizeof(UInt) * 8;
   const int kmin = PREC > (int)maxprec ? PREC - (int)maxprec : 0;
-  unsigned bits = budget, n = 0;
-  encode_planes_from<PREC - 1, UInt, DIMS>(P, bits, n, kmin, wr);
+  unsigned n = 0;
+  encode_planes_from<PREC - 1, UInt, DIMS>(P, n, kmin, wr);
 }
 
-// decode.c:288-321.  Runs of zeros are skipped with one count-trailing-zeros
-// on a 64-bit window; when the budget ends inside a run the reference still
-// deposits a one at the current position, and so do we.
+// decode.c:288-321.  One 64-bit window per group: its bit 0 is the group test,
+// the trailing zeros after it are the run.  `bits` is the budget left; when it
+// ends inside a run the reference still deposits a one at the current
+// position (decode.c:311), and so does the min(z, lim) form below.
 template <int K, typename UInt, int DIMS, typename Reader>
 ZFP_HD void decode_planes_from(planes<UInt, DIMS>& P, unsigned& bits, unsigned& n, int kmin,
                                Reader& rd) {
   if constexpr (K >= 0) {
+    typedef typename plane_word<DIMS>::type PW;
     constexpr unsigned N = 1u << (2 * DIMS);
     if (!bits || K < kmin) return;
-    const unsigned m = umin(n, bits);
-    uint64_t x = rd.peek() & lowmask(m);
-    rd.skip(m);
-    bits -= m;
+    PW x = 0;
+    if (n) {
+      const unsigned m = umin(n, bits);
+      x = (PW)(rd.peek() & lowmask(m));
+      rd.skip(m);
+      bits -= m;
+    }
     while (n < N && bits) {
-      const uint64_t wnd = rd.peek();
-      bits--;
-      if (!(wnd & 1)) {
+      const uint64_t w = rd.peek();
+      if (!(w & 1)) {  // group test "0": plane done
         rd.skip(1);
+        bits--;
         break;
       }
-      const unsigned lim = umin(N - 1 - n, bits);
-      const uint64_t rest = wnd >> 1;
-      const unsigned z = rest ? ctz64(rest) : 64u;
-      unsigned adv;
-      if (z < lim) {
-        adv = z + 1;
-        n += z;
-      } else {
-        adv = lim;
-        n += lim;
-      }
-      rd.skip(1 + adv);
-      bits -= adv;
-      x |= 1ull << n;
+      const unsigned lim = umin(N - 1 - n, bits - 1);  // zeros we may still read
+      const unsigned z = ctz64_or_64(w >> 1);
+      const unsigned adv = umin(z, lim);
+      const unsigned take = 1 + adv + (z < lim ? 1u : 0u);
+      n += adv;
+      x |= (PW)1 << n;
       n++;
+      rd.skip(take);
+      bits -= take;
     }
     P.set(K, x);
     decode_planes_from<K - 1, UInt, DIMS>(P, bits, n, kmin, rd);
@@ -482,8 +551,11 @@ template <> struct fp<double> {
 };
 
 // ---------------------------------------------------------------------------
-// Whole-block encode / decode.  Writer: put(value, n) appends n <= 64 low bits
-// (value has no bits at or above n); finish() pads the block to maxbits.
+// Whole-block encode / decode.
+// Writer: full() is true once the block's maxbits bits are written; while it is
+//   false, put(value, n) appends n <= 64 low bits (value has no bits at or
+//   above n; bits past maxbits are dropped) and zero_bit() appends one 0;
+//   finish() zero-pads the block to maxbits.
 // Reader: peek() returns the next 64 stream bits, skip(n) consumes n <= 64.
 
 template <typename Scalar, int DIMS, typename Writer>
@@ -493,29 +565,43 @@ ZFP_HD void encode_block(const Scalar* f, unsigned maxbits, Writer& wr) {
   typedef typename T::UInt UInt;
   constexpr int N = 1 << (2 * DIMS);
   UInt q[N];
-  unsigned budget = maxbits, maxprec = T::prec;
+  unsigned maxprec = T::prec;
+  (void)maxbits;  // the writer owns the budget
   if constexpr (!T::is_int) {
     // encode.c:187-216
     const int emax = fp<Scalar>::template emax<N>((const Scalar*)f);
     maxprec = precision<DIMS>(emax, T::prec);
     const unsigned e = maxprec ? (unsigned)(emax + T::ebias) : 0u;
     if (!e) {  // all-zero block: a single 0 bit, then padding
-      wr.put(0, 1);
       wr.finish();
       return;
     }
     wr.put(2ull * e + 1, T::ebits + 1);
-    budget = maxbits - (T::ebits + 1);
     const int sh = T::prec - 2 - emax;
-    if (sh > (T::prec == 32 ? 127 : 1023)) {
-      // scale factor overflows to +inf: every product is +-inf or NaN, which the
-      // reference's x86 cast turns into INT_MIN (see oracle/zfp_oracle.c)
+    // When 2^sh overflows (max |x| < 2^-97 for f32, 2^-961 for f64) every
+    // product is +-inf or NaN, which the reference's x86 cast turns into
+    // INT_MIN (see oracle/zfp_oracle.c).  Done with an and-or per value rather
+    // than a branch, so the quantised block reuses the input registers.
+    const bool tiny = sh > (T::prec == 32 ? 127 : 1023);
+    const Scalar s = tiny ? (Scalar)1 : (Scalar)fp<Scalar>::pow2(sh);
+    const UInt keep = tiny ? (UInt)0 : ~(UInt)0;
+    const UInt force = tiny ? (UInt)1 << (T::prec - 1) : (UInt)0;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (sizeof(Scalar) == 4) {
+      // in place (tied operands), so the quantised block reuses the input
+      // registers instead of doubling the block's register footprint
 #pragma unroll
-      for (int i = 0; i < N; i++) q[i] = (UInt)1 << (T::prec - 1);
-    } else {
-      const Scalar s = (Scalar)fp<Scalar>::pow2(sh);
+      for (int i = 0; i < N; i++) {
+        float v = (float)f[i];
+        asm("v_mul_f32 %0, %0, %1\n\tv_cvt_i32_f32 %0, %0\n\tv_and_or_b32 %0, %0, %2, %3"
+            : "+v"(v) : "v"(s), "v"(keep), "v"(force));
+        q[i] = __builtin_bit_cast(UInt, v);
+      }
+    } else
+#endif
+    {
 #pragma unroll
-      for (int i = 0; i < N; i++) q[i] = (UInt)fp<Scalar>::to_int(s * (Scalar)f[i]);
+      for (int i = 0; i < N; i++) q[i] = ((UInt)(Int)(s * (Scalar)f[i]) & keep) | force;  // |s*x| < 2^(p-2)
     }
   } else {
 #pragma unroll
@@ -527,7 +613,7 @@ ZFP_HD void encode_block(const Scalar* f, unsigned maxbits, Writer& wr) {
   permute_fwd<DIMS>(q, u, NB, make_seq<N>());
   planes<UInt, DIMS> P;
   P.load(u);
-  encode_planes<UInt, DIMS>(P, budget, maxprec, wr);
+  encode_planes<UInt, DIMS>(P, maxprec, wr);
   wr.finish();
 }
 

@@ -4,7 +4,7 @@
 // functions the HIP kernels execute on every lane -- serially on the host, so
 // tests/test_emulation.py can check the lane algorithm bit-for-bit against the
 // CPU oracle on a machine without a GPU.  It is never part of the product: the
-// shipped codec path is the HIP kernels in codec_kernels.hip.
+// shipped codec path is the HIP kernels in cuzfp_amd/csrc/kernels.hpp.
 //
 // Raster / padding / stream layout are restated here in the simplest form (the
 // kernels' coalesced gathers and LDS staging are tested on the GPU itself).
@@ -16,16 +16,25 @@
 
 namespace {
 
+// Writes each block at its absolute offset into the zeroed stream, dropping
+// bits past the block's maxbits (the device writers drop them by never
+// flushing a word beyond the block).
 struct HostWriter {
   uint64_t* s;
-  size_t pos;
+  size_t pos, end;
+  bool full() const { return pos >= end; }
   void put(uint64_t v, unsigned n) {
+    if (pos + n > end) {
+      n = (unsigned)(end - pos);
+      v &= cuzfp::lowmask(n);
+    }
     if (!n) return;
     const unsigned sh = pos & 63;
     s[pos >> 6] |= v << sh;
     if (sh + n > 64) s[(pos >> 6) + 1] |= v >> (64 - sh);
     pos += n;
   }
+  void zero_bit() { pos++; }
   void finish() {}
 };
 
@@ -72,7 +81,7 @@ size_t run(bool enc, unsigned nx, unsigned ny, unsigned nz, long long sx, long l
     Scalar f[N];
     if (enc) {
       for (int i = 0; i < N; i++) f[i] = data[off[i]];
-      HostWriter wr{stream, b * (size_t)maxbits};
+      HostWriter wr{stream, b * (size_t)maxbits, (b + 1) * (size_t)maxbits};
       cuzfp::encode_block<Scalar, DIMS>(f, maxbits, wr);
     } else {
       HostReader rd{stream, words, b * (size_t)maxbits};

@@ -52,8 +52,11 @@ def test_sanity_ramp(dims, dtype, cuda, restatement):
     a = np.arange(np.prod(shape), dtype=dtype).reshape(shape)
     mb = cz.rate_to_maxbits(8, dtype, dims, wra=dims == 3)
     words, y = _gpu_roundtrip(a, mb, cuda)
-    assert np.array_equal(words, restatement.compress(a, mb))
-    assert np.array_equal(y.astype(np.int64), a.astype(np.int64))
+    ref = restatement.compress(a, mb)
+    assert np.array_equal(words, ref)
+    assert np.array_equal(y, restatement.decompress(ref, shape, dtype, mb))
+    if dtype == np.float32:  # the reference's assertion (f32 only there)
+        assert np.array_equal(y.astype(np.int64), a.astype(np.int64))
 
 
 @pytest.mark.parametrize("dims", [1, 2, 3])
@@ -160,39 +163,51 @@ def test_int_fields(cuda, restatement, dims, dtype):
 
 
 def test_strided_views(cuda, restatement):
-    """Non-contiguous device views (positive and negative strides) vs the
-    restatement with the same strides (zfp honours sx/sy/sz; cuZFP ignored them)."""
+    """Non-contiguous device views vs the restatement with the same strides (zfp
+    honours sx/sy/sz; cuZFP ignored them).  torch views give positive strides;
+    negative strides go through the C-ABI with a hand-made base pointer."""
     import ctypes
     import torch
     rng = np.random.default_rng(21)
     base = rng.standard_normal((16, 12, 26)).astype(np.float32)
     tb = torch.from_numpy(base).to(cuda)
-    for sl in [(slice(None, None, 2), slice(None), slice(1, 19)),
-               (slice(None), slice(None, None, -1), slice(None, None, -2)),
-               (slice(3, 14), slice(2, 11), slice(None, None, 3))]:
-        view_t = tb[sl]
+    mb = 384
+    cases = [((slice(None, None, 2), slice(None), slice(1, 19)), None),
+             ((slice(3, 14), slice(2, 11), slice(None, None, 3)), None),
+             ((slice(None), slice(None, None, -1), slice(None, None, -2)), "negative")]
+    lib = cz.library()
+    for sl, kind in cases:
         view_n = base[sl]
         nz, ny, nx = view_n.shape
         st = tuple(s // 4 for s in view_n.strides[::-1])
-        mb = 384
+        off = (view_n.__array_interface__["data"][0] - base.__array_interface__["data"][0]) // 4
         cap = restatement.stream_bytes(view_n.shape, mb) + 64
         ref = np.zeros(cap // 8, np.uint64)
         n = restatement.lib.oracle_compress(3, nx, ny, nz, st[0], st[1], st[2], mb,
                                             view_n.__array_interface__["data"][0], ref.ctypes.data, cap)
-        words = cz.encode(view_t, mb)
+        ref = ref[: n // 8]
+        if kind is None:
+            words = cz.encode(tb[sl], mb)
+        else:
+            words = torch.empty(n // 8, dtype=torch.int64, device=cuda)
+            got = ctypes.c_size_t(0)
+            rc = lib.cuzfp_hip_encode(tb.data_ptr() + 4 * off, 3, nx, ny, nz, st[0], st[1], st[2], mb,
+                                      words.data_ptr(), n, ctypes.byref(got), None)
+            assert rc == 0
         torch.cuda.synchronize()
-        assert np.array_equal(words.cpu().numpy().view(np.uint64), ref[: n // 8])
+        assert np.array_equal(words.cpu().numpy().view(np.uint64), ref), kind
         # decode into a strided destination, leaving the gaps untouched
         dst = torch.full_like(tb, -7.0)
-        cz.decode(words, view_t.shape, view_t.dtype, mb, out=dst[sl])
+        rc = lib.cuzfp_hip_decode(words.data_ptr(), n, 3, nx, ny, nz, st[0], st[1], st[2], mb,
+                                  dst.data_ptr() + 4 * off, None)
+        assert rc == 0
         torch.cuda.synchronize()
         got = dst.cpu().numpy()
-        want = restatement.decompress(ref[: n // 8], view_n.shape, np.float32, mb)
+        want = restatement.decompress(ref, view_n.shape, np.float32, mb)
         assert np.array_equal(got[sl], want)
         mask = np.ones(base.shape, bool)
         mask[sl] = False
         assert np.all(got[mask] == -7.0)
-    del ctypes
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])

@@ -34,16 +34,16 @@ for s in $STEPS; do
       ok_or_stop $? bench64; cat "$OUT/bench_f64_$TAG.json" ;;
     prof)
       rm -rf "$OUT/prof_$TAG"
-      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run -- \
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o run -- \
         python bench.py --steps 20 --no-cpu-baseline --no-host-path > "$OUT/prof_bench_$TAG.json" 2>&1
       ok_or_stop $? prof
       find "$OUT/prof_$TAG" -name "*kernel_stats.csv" -exec head -8 {} \; ;;
     pmc)
       rm -rf "$OUT/pmc_$TAG"
-      timeout -k 10 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/pmc_$TAG/fetch" -o run -- \
+      timeout -k 10 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_$TAG/fetch" -o run -- \
         python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-host-path > /dev/null 2>&1
       ok_or_stop $? pmc_fetch
-      timeout -k 10 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/pmc_$TAG/write" -o run -- \
+      timeout -k 10 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_$TAG/write" -o run -- \
         python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-host-path > /dev/null 2>&1
       ok_or_stop $? pmc_write ;;
     *) echo "unknown step $s" ;;
