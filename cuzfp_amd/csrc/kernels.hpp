@@ -102,25 +102,28 @@ struct LdsBitWriter {
   }
 };
 
-// 128-bit window over the wave's LDS stream image.
+// 128-bit window over the wave's LDS stream image, plus one word prefetched,
+// so a refill never waits on the LDS read it issues.
 struct LdsReader {
   const uint64_t* lds;
-  uint64_t w0, w1;
+  uint64_t w0, w1, w2;
   uint32_t s, next;
   __device__ __forceinline__ void init(uint32_t bitpos) {
     const uint32_t wi = bitpos >> 6;
     s = bitpos & 63;
     w0 = lds[wi];
     w1 = lds[wi + 1];
-    next = wi + 2;
+    w2 = lds[wi + 2];
+    next = wi + 3;
   }
-  __device__ __forceinline__ uint64_t peek() const { return s ? (w0 >> s) | (w1 << (64 - s)) : w0; }
+  __device__ __forceinline__ uint64_t peek() const { return (w0 >> s) | ((w1 << 1) << (63 - s)); }
   __device__ __forceinline__ void skip(unsigned n) {
     s += n;
     if (s >= 64) {
       s -= 64;
       w0 = w1;
-      w1 = lds[next++];
+      w1 = w2;
+      w2 = lds[next++];
     }
   }
 };
@@ -295,7 +298,7 @@ __global__ __launch_bounds__(kLanes, 4) void zfp_decode(const uint64_t* __restri
   } else {
     for (uint32_t j = lane; j < nwords; j += kLanes) lds[j] = in[j];
   }
-  if (lane < 2) lds[nwords + lane] = 0;  // reader look-ahead slack
+  if (lane < 3) lds[nwords + lane] = 0;  // reader look-ahead slack
   __syncthreads();
   if (b < g.nblocks) {
     LdsReader rd;
@@ -338,7 +341,7 @@ int launch_decode_t(const uint64_t* stream, const Geometry& g, bool fast, void* 
   Geometry gg = g;
   gg.wave0 = wave0;
   gg.vec_io = (g.maxbits % 2 == 0) && ((uintptr_t)stream % 16 == 0);
-  const size_t lds = ((size_t)g.maxbits + 2) * 8;
+  const size_t lds = ((size_t)g.maxbits + 3) * 8;
   Scalar* d = (Scalar*)data;
   if (fast)
     hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, true>), dim3(nwaves), dim3(kLanes), lds, st, stream, gg, d);

@@ -444,7 +444,9 @@ ZFP_HD void encode_planes(const planes<UInt, DIMS>& P, unsigned maxprec, Writer&
 // decode.c:288-321.  One 64-bit window per group: its bit 0 is the group test,
 // the trailing zeros after it are the run.  `bits` is the budget left; when it
 // ends inside a run the reference still deposits a one at the current
-// position (decode.c:311), and so does the min(z, lim) form below.
+// position (decode.c:311), and so does the min(z, lim) form below.  The group
+// step is branch-free (selects on the group bit), so a wave only pays for its
+// longest plane, not for per-lane if/else paths.
 template <int K, typename UInt, int DIMS, typename Reader>
 ZFP_HD void decode_planes_from(planes<UInt, DIMS>& P, unsigned& bits, unsigned& n, int kmin,
                                Reader& rd) {
@@ -459,22 +461,20 @@ ZFP_HD void decode_planes_from(planes<UInt, DIMS>& P, unsigned& bits, unsigned& 
       rd.skip(m);
       bits -= m;
     }
-    while (n < N && bits) {
+    bool more = n < N && bits;
+    while (more) {
       const uint64_t w = rd.peek();
-      if (!(w & 1)) {  // group test "0": plane done
-        rd.skip(1);
-        bits--;
-        break;
-      }
+      const bool g = w & 1;                             // group test
       const unsigned lim = umin(N - 1 - n, bits - 1);  // zeros we may still read
       const unsigned z = ctz64_or_64(w >> 1);
       const unsigned adv = umin(z, lim);
-      const unsigned take = 1 + adv + (z < lim ? 1u : 0u);
-      n += adv;
-      x |= (PW)1 << n;
-      n++;
+      const unsigned nn = n + adv;                      // position of the one
+      const unsigned take = g ? 1 + adv + (z < lim ? 1u : 0u) : 1u;
+      x |= (PW)g << nn;
+      n = g ? nn + 1 : n;
       rd.skip(take);
       bits -= take;
+      more = g && n < N && bits;
     }
     P.set(K, x);
     decode_planes_from<K - 1, UInt, DIMS>(P, bits, n, kmin, rd);
@@ -577,31 +577,43 @@ ZFP_HD void encode_block(const Scalar* f, unsigned maxbits, Writer& wr) {
       return;
     }
     wr.put(2ull * e + 1, T::ebits + 1);
-    const int sh = T::prec - 2 - emax;
-    // When 2^sh overflows (max |x| < 2^-97 for f32, 2^-961 for f64) every
-    // product is +-inf or NaN, which the reference's x86 cast turns into
-    // INT_MIN (see oracle/zfp_oracle.c).  Done with an and-or per value rather
-    // than a branch, so the quantised block reuses the input registers.
-    const bool tiny = sh > (T::prec == 32 ? 127 : 1023);
-    const Scalar s = tiny ? (Scalar)1 : (Scalar)fp<Scalar>::pow2(sh);
-    const UInt keep = tiny ? (UInt)0 : ~(UInt)0;
-    const UInt force = tiny ? (UInt)1 << (T::prec - 1) : (UInt)0;
+    // q = (Int)(2^sh * x) with the reference's x86 cast: NaN or |y| >= 2^(p-1)
+    // gives INT_MIN.  That happens when 2^sh overflows (max |x| < 2^-97 for
+    // f32, 2^-961 for f64) and in blocks holding inf or NaN; see
+    // oracle/zfp_oracle.c.
+    const Scalar s = (Scalar)fp<Scalar>::pow2(T::prec - 2 - emax);
 #if defined(__HIP_DEVICE_COMPILE__)
-    if constexpr (sizeof(Scalar) == 4) {
-      // in place (tied operands), so the quantised block reuses the input
-      // registers instead of doubling the block's register footprint
+    if constexpr (sizeof(Scalar) == 4 && N % 2 == 0) {
+      // Two values per statement, in place (tied operands), so the quantised
+      // block reuses the input registers instead of doubling the block's
+      // register footprint.  Each compare result is read >= 2 instructions
+      // after it is written (VALU SGPR/VCC write -> v_cndmask read).
+      const float lim = 2147483648.0f;
+      const uint32_t imin = 0x80000000u;
 #pragma unroll
-      for (int i = 0; i < N; i++) {
-        float v = (float)f[i];
-        asm("v_mul_f32 %0, %0, %1\n\tv_cvt_i32_f32 %0, %0\n\tv_and_or_b32 %0, %0, %2, %3"
-            : "+v"(v) : "v"(s), "v"(keep), "v"(force));
-        q[i] = __builtin_bit_cast(UInt, v);
+      for (int i = 0; i < N; i += 2) {
+        float a = (float)f[i], b = (float)f[i + 1];
+        uint64_t m;
+        uint32_t t;
+        asm("v_mul_f32 %0, %0, %4\n\t"
+            "v_mul_f32 %1, %1, %4\n\t"
+            "v_cmp_gt_f32_e64 vcc, %5, |%0|\n\t"
+            "v_cmp_gt_f32_e64 %2, %5, |%1|\n\t"
+            "v_cvt_i32_f32 %3, %0\n\t"
+            "v_cndmask_b32 %0, %6, %3, vcc\n\t"
+            "v_cvt_i32_f32 %3, %1\n\t"
+            "v_cndmask_b32_e64 %1, %6, %3, %2"
+            : "+v"(a), "+v"(b), "=&s"(m), "=&v"(t)
+            : "v"(s), "v"(lim), "v"(imin)
+            : "vcc");
+        q[i] = __builtin_bit_cast(UInt, a);
+        q[i + 1] = __builtin_bit_cast(UInt, b);
       }
     } else
 #endif
     {
 #pragma unroll
-      for (int i = 0; i < N; i++) q[i] = ((UInt)(Int)(s * (Scalar)f[i]) & keep) | force;  // |s*x| < 2^(p-2)
+      for (int i = 0; i < N; i++) q[i] = (UInt)fp<Scalar>::to_int(s * (Scalar)f[i]);
     }
   } else {
 #pragma unroll
