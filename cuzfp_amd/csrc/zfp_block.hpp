@@ -353,12 +353,22 @@ template <> struct plane_word<3> { typedef uint64_t type; };
 ZFP_HD unsigned ctz(uint32_t x) { return (unsigned)__builtin_ctz(x); }  // x != 0
 ZFP_HD unsigned ctz(uint64_t x) { return (unsigned)__builtin_ctzll(x); }
 
-// count of trailing zeros, 64 for x == 0 (v_ffbl_b32 returns ~0 for a zero word)
+// count of trailing zeros of x; any value >= 64 when x == 0
 ZFP_HD unsigned ctz64_or_64(uint64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  // v_ffbl_b32 returns ~0 for a zero word: min(lo, hi | 32) is the 64-bit
+  // count (or ~0) in four instructions, without the compiler's zero checks
+  unsigned lo, hi;
+  asm("v_ffbl_b32 %0, %1" : "=v"(lo) : "v"((uint32_t)x));
+  asm("v_ffbl_b32 %0, %1" : "=v"(hi) : "v"((uint32_t)(x >> 32)));
+  hi |= 32u;
+  return lo < hi ? lo : hi;
+#else
   const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
   const unsigned zl = lo ? (unsigned)__builtin_ctz(lo) : 64u;
   const unsigned zh = hi ? 32u + (unsigned)__builtin_ctz(hi) : 64u;
   return zl < zh ? zl : zh;
+#endif
 }
 
 // The plane loop is unrolled by template recursion so that plane K is a
@@ -461,20 +471,31 @@ ZFP_HD void decode_planes_from(planes<UInt, DIMS>& P, unsigned& bits, unsigned& 
       rd.skip(m);
       bits -= m;
     }
-    bool more = n < N && bits;
-    while (more) {
-      const uint64_t w = rd.peek();
-      const bool g = w & 1;                             // group test
-      const unsigned lim = umin(N - 1 - n, bits - 1);  // zeros we may still read
-      const unsigned z = ctz64_or_64(w >> 1);
-      const unsigned adv = umin(z, lim);
-      const unsigned nn = n + adv;                      // position of the one
-      const unsigned take = g ? 1 + adv + (z < lim ? 1u : 0u) : 1u;
-      x |= (PW)g << nn;
-      n = g ? nn + 1 : n;
-      rd.skip(take);
-      bits -= take;
-      more = g && n < N && bits;
+    if (n < N && bits) {
+      // leading group test: a "0" ends the plane at once, without a loop trip
+      const bool g0 = rd.peek() & 1;
+      rd.skip(1);
+      bits--;
+      bool more = g0;
+      // one trip per new one: the run of zeros, the one (unless implied at
+      // position N-1) and the following group test, all from one window
+      while (more) {
+        const uint64_t w = rd.peek();
+        const unsigned lim = umin(N - 1 - n, bits);   // zeros we may still read
+        const unsigned z = ctz64_or_64(w);            // zeros before the one
+        const bool found = z < lim;                   // the one is read, not implied
+        const unsigned adv = found ? z : lim;
+        n += adv;
+        x |= (PW)1 << n;
+        n++;
+        const unsigned used = adv + (found ? 1u : 0u);
+        // the group test after a read one: "1" = more ones follow
+        const bool gt = found && used < bits && n < N && ((w >> used) & 1);
+        const unsigned take = used + ((found && used < bits && n < N) ? 1u : 0u);
+        rd.skip(take);
+        bits -= take;
+        more = gt;  // with bits == 0 the next trip deposits at n (decode.c:311)
+      }
     }
     P.set(K, x);
     decode_planes_from<K - 1, UInt, DIMS>(P, bits, n, kmin, rd);

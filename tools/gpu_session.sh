@@ -46,6 +46,15 @@ for s in $STEPS; do
       timeout -k 10 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_$TAG/write" -o run -- \
         python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-host-path > /dev/null 2>&1
       ok_or_stop $? pmc_write ;;
+    counters)
+      # instruction mix / stall counters of the codec kernels (one --pmc pass per group)
+      i=0
+      for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY" "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SALU SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM" "SQ_INSTS_VMEM SQ_INSTS_BRANCH SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"; do
+        i=$((i+1))
+        timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d "$OUT/ctr_$TAG/g$i" -o run -- \
+          python tools/kernel_probe.py ${PROBE_ARGS:-} > /dev/null 2>&1
+        ok_or_stop $? counters_g$i
+      done ;;
     *) echo "unknown step $s" ;;
   esac
 done
