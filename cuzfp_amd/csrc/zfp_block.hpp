@@ -254,14 +254,24 @@ ZFP_HD void transpose_tiles(uint32_t* a) {
 // Planes of N = 4^DIMS coefficients held as 32-bit words.  For 32-bit
 // coefficients W = N words; 64-bit coefficients are split into low and high
 // halves (planes 0..31 from the low words, 32..63 from the high words).
+//
+// The words live in vector registers as clang ext_vector_type values of R
+// words (v[h][g][row] = word g*R + row of half h), so the plane coders can
+// index them with a runtime, wave-uniform plane number: the compiler lowers
+// that to s_set_gpr_idx_on + v_mov (VGPR-relative addressing), which keeps the
+// plane loop a loop -- one copy of its body in the instruction cache -- instead
+// of 32 or 64 unrolled copies.  (A runtime index into a plain array, or into a
+// vector wider than 32 registers, would be lowered to scratch memory.)
 template <typename UInt, int DIMS> struct planes {
   static constexpr int N = 1 << (2 * DIMS);
   static constexpr int H = sizeof(UInt) / 4;      // 32-bit halves per value
   static constexpr int R = N < 32 ? N : 32;       // tile height
   static constexpr int G = N / R;                 // row groups (2 for 3D)
-  uint32_t w[H][N];                               // w[half][group*R + row]
+  typedef uint32_t vec __attribute__((ext_vector_type(R)));
+  vec v[H][G];
 
   ZFP_HD void load(const UInt* u) {
+    uint32_t w[H][N];
 #pragma unroll
     for (int i = 0; i < N; i++) {
       w[0][i] = (uint32_t)u[i];
@@ -271,71 +281,64 @@ template <typename UInt, int DIMS> struct planes {
     for (int h = 0; h < H; h++)
 #pragma unroll
       for (int g = 0; g < G; g++) transpose_tiles<R>(&w[h][g * R]);
-    pin();
+#pragma unroll
+    for (int h = 0; h < H; h++)
+#pragma unroll
+      for (int g = 0; g < G; g++)
+#pragma unroll
+        for (int r = 0; r < R; r++) v[h][g][r] = w[h][g * R + r];
   }
 
-  // Materialise every plane word here: without this the compiler sinks the
-  // transpose stages into the plane loop and keeps pre- and post-transpose
-  // copies alive at once, which costs registers (occupancy).
-  // For 64 coefficients each plane is pinned as one 64-bit register pair, the
-  // operand form of the plane coder's 64-bit shifts.
-  ZFP_HD void pin() {
-#if defined(__HIP_DEVICE_COMPILE__)
+  ZFP_HD void store(UInt* u) const {
+    uint32_t w[H][N];
 #pragma unroll
-    for (int h = 0; h < H; h++) {
-      if constexpr (N == 64) {
+    for (int h = 0; h < H; h++)
 #pragma unroll
-        for (int c = 0; c < 32; c++) {
-          uint64_t v = (uint64_t)w[h][c] | ((uint64_t)w[h][32 + c] << 32);
-          asm volatile("" : "+v"(v));
-          w[h][c] = (uint32_t)v;
-          w[h][32 + c] = (uint32_t)(v >> 32);
-        }
-      } else {
+      for (int g = 0; g < G; g++)
 #pragma unroll
-        for (int i = 0; i < N; i++) asm volatile("" : "+v"(w[h][i]));
-      }
-    }
-#endif
-  }
-
-  ZFP_HD void store(UInt* u) {
+        for (int r = 0; r < R; r++) w[h][g * R + r] = v[h][g][r];
 #pragma unroll
     for (int h = 0; h < H; h++)
 #pragma unroll
       for (int g = 0; g < G; g++) transpose_tiles<R>(&w[h][g * R]);
 #pragma unroll
     for (int i = 0; i < N; i++) {
-      uint64_t v = w[0][i];
-      if (H == 2) v |= (uint64_t)w[H - 1][i] << 32;
-      u[i] = (UInt)v;
+      uint64_t x = w[0][i];
+      if (H == 2) x |= (uint64_t)w[H - 1][i] << 32;
+      u[i] = (UInt)x;
     }
-  }
-
-  // plane k as an N-bit word (bit i = bit k of coefficient i); k compile-time
-  // after unrolling.
-  ZFP_HD uint64_t get(int k) const {
-    const int h = k >> 5, c = k & 31;
-    if (N == 64) return (uint64_t)w[h][c] | ((uint64_t)w[h][32 + c] << 32);
-    return (w[h][c % R] >> (R * (c / R))) & (uint32_t)lowmask(R);
   }
 
   ZFP_HD void zero() {
 #pragma unroll
     for (int h = 0; h < H; h++)
 #pragma unroll
-      for (int i = 0; i < N; i++) w[h][i] = 0;
+      for (int g = 0; g < G; g++) v[h][g] = (vec)0u;
   }
 
-  // deposit plane k (bits beyond N are zero)
-  ZFP_HD void set(int k, uint64_t x) {
-    const int h = k >> 5, c = k & 31;
-    if (N == 64) {
-      w[h][c] = (uint32_t)x;
-      w[h][32 + c] = (uint32_t)(x >> 32);
+  // plane c (0..31) of half h as an N-bit word (bit i = that bit of
+  // coefficient i); h is a compile-time constant, c may be a runtime value
+  // (wave-uniform in the kernels).
+  template <int h> ZFP_HD uint64_t get(int c) const {
+    if constexpr (N == 64) return (uint64_t)v[h][0][c] | ((uint64_t)v[h][1][c] << 32);
+    else return (v[h][0][c % R] >> (R * (c / R))) & (uint32_t)lowmask(R);
+  }
+  ZFP_HD uint64_t get(int k) const {  // k compile-time after unrolling
+    return (k >> 5) ? get<H - 1>(k & 31) : get<0>(k & 31);
+  }
+
+  // deposit plane c of half h (bits beyond N are zero; the plane was zero)
+  template <int h> ZFP_HD void set(int c, uint64_t x) {
+    if constexpr (N == 64) {
+      v[h][0][c] = (uint32_t)x;
+      v[h][1][c] = (uint32_t)(x >> 32);
     } else {
-      w[h][c % R] |= (uint32_t)x << (R * (c / R));
+      v[h][0][c % R] |= (uint32_t)x << (R * (c / R));
     }
+  }
+  ZFP_HD void set(int k, uint64_t x) {
+    if (k >> 5) set<H - 1>(k & 31, x);
+    else set<0>(k & 31, x);
   }
 };
 
@@ -371,84 +374,97 @@ ZFP_HD unsigned ctz64_or_64(uint64_t x) {
 #endif
 }
 
-// The plane loop is unrolled by template recursion so that plane K is a
-// compile-time register index (a runtime-indexed plane array would live in
-// scratch memory).  A lane whose block is full returns; the wave walks on only
-// while some lane still has bits left.
-//
-// Encoder plane step.  With n coefficients already significant the plane's code
-// is: its first n bits verbatim, then for every further one bit at position p
-// a group "1" + the zeros before p + that one (implied, so omitted, when
-// p = N-1), then a closing "0" group test if positions remain.  Positions are
-// absolute (r keeps the not-yet-coded ones), so every group costs one ctz, one
-// put and one r &= r - 1.  The writer is never asked to clip: it reports
-// full() once the block's maxbits are written and the loop stops there, so the
-// stream is exactly the reference's budget-truncated prefix.
-template <int K, typename UInt, int DIMS, typename Writer>
-ZFP_HD void encode_planes_from(const planes<UInt, DIMS>& P, unsigned& n, int kmin, Writer& wr) {
-  if constexpr (K >= 0) {
-    typedef typename plane_word<DIMS>::type PW;
-    constexpr unsigned N = 1u << (2 * DIMS);
-    if (wr.full() || K < kmin) return;
-    const PW x = (PW)P.get(K);
-    // verbatim part
-    if (n) wr.put(x & (PW)lowmask(n), n);
-    // new ones, in the frame of the first not-yet-significant coefficient
-    const PW r = n < N ? (PW)(x >> n) : (PW)0;
-    if (!r) {
-      if (n < N && !wr.full()) wr.zero_bit();  // group test "0"
-    } else if (!wr.full()) {
-      // With t new ones at relative positions p_0 < ... < p_{t-1} the group
-      // code is  1 (z_0 zeros) 1 1 (z_1 zeros) 1 1 ... (z_{t-1} zeros) 1 0,
-      // i.e. "1" followed by the segment up to p_{t-1} with every one doubled,
-      // the last one's partner being the closing "0" -- or, when the last one
-      // sits at position N-1, both its bit and the closing test omitted.  The
-      // j-th one therefore lands at bit p_j + j + 1 (and its partner at + 2):
-      // F collects those positions with one shift per one, no branches on the
-      // stream.
-      const unsigned pt = (unsigned)(8 * sizeof(PW) - 1) - (unsigned)(sizeof(PW) == 8 ? __builtin_clzll((uint64_t)r) : __builtin_clz((uint32_t)r));
-      const unsigned t = (unsigned)(sizeof(PW) == 8 ? __builtin_popcountll((uint64_t)r) : __builtin_popcount((uint32_t)r));
-      const unsigned qmax = pt + t - 1;  // F position of the last one
-      const bool last_n = pt + n == N - 1;
-      if (qmax <= 61) {
-        uint64_t F = 0;
-        PW rr = r;
-        unsigned j = 0;
-        while (rr) {
-          const PW low = rr & (PW)(0 - rr);
-          F |= (uint64_t)low << j;
-          rr ^= low;
-          j++;
-        }
-        const unsigned L = qmax + (last_n ? 1u : 3u);
-        const uint64_t G = (1ull | (F << 1) | (F << 2)) & lowmask(last_n ? L : L - 1);
-        wr.put(G, L);
-        n += pt + 1;
-      } else {
-        // dense plane (many ones early in a wide block): one put per group
-        PW rest = r;
-        unsigned base = n;
-        while (rest && !wr.full()) {
-          const unsigned p = ctz(rest);
-          const bool last = base + p == N - 1;
-          const unsigned z = p - (n - base);
-          wr.put(last ? 1ull : (1ull | (2ull << z)), z + (last ? 1u : 2u));
-          n = base + p + 1;
-          rest &= rest - 1;
-        }
-        if (n < N && !wr.full()) wr.zero_bit();
+// Encoder plane step.  With n coefficients already significant the plane's
+// code is: its first n bits verbatim, then for every further one bit at
+// position p a group "1" + the zeros before p + that one (implied, so omitted,
+// when p = N-1), then a closing "0" group test if positions remain.  The
+// writer is never asked to clip: it reports full() once the block's maxbits
+// are written and the plane loop stops there, so the stream is exactly the
+// reference's budget-truncated prefix.
+template <int DIMS, typename PW, typename Writer>
+ZFP_HD void encode_plane(PW x, unsigned& n, Writer& wr) {
+  constexpr unsigned N = 1u << (2 * DIMS);
+  // verbatim part
+  if (n) wr.put(x & (PW)lowmask(n), n);
+  // new ones, in the frame of the first not-yet-significant coefficient
+  const PW r = n < N ? (PW)(x >> n) : (PW)0;
+  if (!r) {
+    if (n < N && !wr.full()) wr.zero_bit();  // group test "0"
+  } else if (!wr.full()) {
+    // With t new ones at relative positions p_0 < ... < p_{t-1} the group
+    // code is  1 (z_0 zeros) 1 1 (z_1 zeros) 1 1 ... (z_{t-1} zeros) 1 0,
+    // i.e. "1" followed by the segment up to p_{t-1} with every one doubled,
+    // the last one's partner being the closing "0" -- or, when the last one
+    // sits at position N-1, both its bit and the closing test omitted.  The
+    // j-th one therefore lands at bit p_j + j + 1 (and its partner at + 2):
+    // F collects those positions with one shift per one, no branches on the
+    // stream.
+    const unsigned pt = (unsigned)(8 * sizeof(PW) - 1) - (unsigned)(sizeof(PW) == 8 ? __builtin_clzll((uint64_t)r) : __builtin_clz((uint32_t)r));
+    const unsigned t = (unsigned)(sizeof(PW) == 8 ? __builtin_popcountll((uint64_t)r) : __builtin_popcount((uint32_t)r));
+    const unsigned qmax = pt + t - 1;  // F position of the last one
+    const bool last_n = pt + n == N - 1;
+    if (qmax <= 61) {
+      uint64_t F = 0;
+      PW rr = r;
+      unsigned j = 0;
+      while (rr) {
+        const PW low = rr & (PW)(0 - rr);
+        F |= (uint64_t)low << j;
+        rr ^= low;
+        j++;
       }
+      const unsigned L = qmax + (last_n ? 1u : 3u);
+      const uint64_t G = (1ull | (F << 1) | (F << 2)) & lowmask(last_n ? L : L - 1);
+      wr.put(G, L);
+      n += pt + 1;
+    } else {
+      // dense plane (many ones early in a wide block): one put per group
+      PW rest = r;
+      unsigned base = n;
+      while (rest && !wr.full()) {
+        const unsigned p = ctz(rest);
+        const bool last = base + p == N - 1;
+        const unsigned z = p - (n - base);
+        wr.put(last ? 1ull : (1ull | (2ull << z)), z + (last ? 1u : 2u));
+        n = base + p + 1;
+        rest &= rest - 1;
+      }
+      if (n < N && !wr.full()) wr.zero_bit();
     }
-    encode_planes_from<K - 1, UInt, DIMS>(P, n, kmin, wr);
   }
+}
+
+// Plane loop, most significant plane first (encode.c:133-150).  The plane
+// number is a runtime value but the same on every lane of the wave (lanes whose
+// block is full drop out; the wave walks on while any lane has bits left), so
+// P.get() is VGPR-relative addressing, not scratch.
+// The plane number of a plane loop: the same on every active lane, so say so
+// (the loops' exits are per lane, which makes the compiler treat the counter as
+// divergent and wrap each indexed access in a readfirstlane loop).
+ZFP_HD int uniform(int c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_readfirstlane(c);
+#else
+  return c;
+#endif
 }
 
 template <typename UInt, int DIMS, typename Writer>
 ZFP_HD void encode_planes(const planes<UInt, DIMS>& P, unsigned maxprec, Writer& wr) {
+  typedef typename plane_word<DIMS>::type PW;
   constexpr int PREC = (int)sizeof(UInt) * 8;
   const int kmin = PREC > (int)maxprec ? PREC - (int)maxprec : 0;
   unsigned n = 0;
-  encode_planes_from<PREC - 1, UInt, DIMS>(P, n, kmin, wr);
+  if constexpr (PREC == 64) {
+    for (int c = 31; c >= 0 && c + 32 >= kmin; c--) {
+      if (wr.full()) return;
+      encode_plane<DIMS>((PW)P.template get<1>(uniform(c)), n, wr);
+    }
+  }
+  for (int c = 31; c >= 0 && c >= kmin; c--) {
+    if (wr.full()) return;
+    encode_plane<DIMS>((PW)P.template get<0>(uniform(c)), n, wr);
+  }
 }
 
 // decode.c:288-321.  One 64-bit window per group: its bit 0 is the group test,
@@ -457,58 +473,62 @@ ZFP_HD void encode_planes(const planes<UInt, DIMS>& P, unsigned maxprec, Writer&
 // position (decode.c:311), and so does the min(z, lim) form below.  The group
 // step is branch-free (selects on the group bit), so a wave only pays for its
 // longest plane, not for per-lane if/else paths.
-template <int K, typename UInt, int DIMS, typename Reader>
-ZFP_HD void decode_planes_from(planes<UInt, DIMS>& P, unsigned& bits, unsigned& n, int kmin,
-                               Reader& rd) {
-  if constexpr (K >= 0) {
-    typedef typename plane_word<DIMS>::type PW;
-    constexpr unsigned N = 1u << (2 * DIMS);
-    if (!bits || K < kmin) return;
-    PW x = 0;
-    if (n) {
-      const unsigned m = umin(n, bits);
-      x = (PW)(rd.peek() & lowmask(m));
-      rd.skip(m);
-      bits -= m;
-    }
-    if (n < N && bits) {
-      // leading group test: a "0" ends the plane at once, without a loop trip
-      const bool g0 = rd.peek() & 1;
-      rd.skip(1);
-      bits--;
-      bool more = g0;
-      // one trip per new one: the run of zeros, the one (unless implied at
-      // position N-1) and the following group test, all from one window
-      while (more) {
-        const uint64_t w = rd.peek();
-        const unsigned lim = umin(N - 1 - n, bits);   // zeros we may still read
-        const unsigned z = ctz64_or_64(w);            // zeros before the one
-        const bool found = z < lim;                   // the one is read, not implied
-        const unsigned adv = found ? z : lim;
-        n += adv;
-        x |= (PW)1 << n;
-        n++;
-        const unsigned used = adv + (found ? 1u : 0u);
-        // the group test after a read one: "1" = more ones follow
-        const bool gt = found && used < bits && n < N && ((w >> used) & 1);
-        const unsigned take = used + ((found && used < bits && n < N) ? 1u : 0u);
-        rd.skip(take);
-        bits -= take;
-        more = gt;  // with bits == 0 the next trip deposits at n (decode.c:311)
-      }
-    }
-    P.set(K, x);
-    decode_planes_from<K - 1, UInt, DIMS>(P, bits, n, kmin, rd);
+template <int DIMS, typename PW, typename Reader>
+ZFP_HD PW decode_plane(unsigned& bits, unsigned& n, Reader& rd) {
+  constexpr unsigned N = 1u << (2 * DIMS);
+  PW x = 0;
+  if (n) {
+    const unsigned m = umin(n, bits);
+    x = (PW)(rd.peek() & lowmask(m));
+    rd.skip(m);
+    bits -= m;
   }
+  if (n < N && bits) {
+    // leading group test: a "0" ends the plane at once, without a loop trip
+    const bool g0 = rd.peek() & 1;
+    rd.skip(1);
+    bits--;
+    bool more = g0;
+    // one trip per new one: the run of zeros, the one (unless implied at
+    // position N-1) and the following group test, all from one window
+    while (more) {
+      const uint64_t w = rd.peek();
+      const unsigned lim = umin(N - 1 - n, bits);   // zeros we may still read
+      const unsigned z = ctz64_or_64(w);            // zeros before the one
+      const bool found = z < lim;                   // the one is read, not implied
+      const unsigned adv = found ? z : lim;
+      n += adv;
+      x |= (PW)1 << n;
+      n++;
+      const unsigned used = adv + (found ? 1u : 0u);
+      // the group test after a read one: "1" = more ones follow
+      const bool gt = found && used < bits && n < N && ((w >> used) & 1);
+      const unsigned take = used + ((found && used < bits && n < N) ? 1u : 0u);
+      rd.skip(take);
+      bits -= take;
+      more = gt;  // with bits == 0 the next trip deposits at n (decode.c:311)
+    }
+  }
+  return x;
 }
 
 template <typename UInt, int DIMS, typename Reader>
 ZFP_HD void decode_planes(planes<UInt, DIMS>& P, unsigned budget, unsigned maxprec, Reader& rd) {
+  typedef typename plane_word<DIMS>::type PW;
   constexpr int PREC = (int)sizeof(UInt) * 8;
   const int kmin = PREC > (int)maxprec ? PREC - (int)maxprec : 0;
   unsigned bits = budget, n = 0;
   P.zero();
-  decode_planes_from<PREC - 1, UInt, DIMS>(P, bits, n, kmin, rd);
+  if constexpr (PREC == 64) {
+    for (int c = 31; c >= 0 && c + 32 >= kmin; c--) {
+      if (!bits) return;
+      P.template set<1>(uniform(c), decode_plane<DIMS, PW>(bits, n, rd));
+    }
+  }
+  for (int c = 31; c >= 0 && c >= kmin; c--) {
+    if (!bits) return;
+    P.template set<0>(uniform(c), decode_plane<DIMS, PW>(bits, n, rd));
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -644,9 +664,26 @@ ZFP_HD void encode_block(const Scalar* f, unsigned maxbits, Writer& wr) {
   UInt u[N];
   constexpr UInt NB = nbmask<UInt>::value;
   permute_fwd<DIMS>(q, u, NB, make_seq<N>());
+#if defined(CUZFP_PROBE) && CUZFP_PROBE > 0
+  // timing probes (tools/probe.py; never built into the product library):
+  // 1 = no plane coder, 2 = no transpose either
+  uint64_t acc = 0;
+#if CUZFP_PROBE == 1
+  planes<UInt, DIMS> P;
+  P.load(u);
+#pragma unroll
+  for (int k = 0; k < (int)sizeof(UInt) * 8; k++) acc ^= (uint64_t)P.get(k) << (k & 7);
+#else
+#pragma unroll
+  for (int i = 0; i < N; i++) acc ^= (uint64_t)u[i] << (i & 31);
+#endif
+  wr.put(acc, 64);
+  (void)maxprec;
+#else
   planes<UInt, DIMS> P;
   P.load(u);
   encode_planes<UInt, DIMS>(P, maxprec, wr);
+#endif
   wr.finish();
 }
 
@@ -671,10 +708,29 @@ ZFP_HD void decode_block(Scalar* f, unsigned maxbits, Reader& rd) {
     maxprec = precision<DIMS>(emax, T::prec);
     budget = maxbits - (T::ebits + 1);
   }
+  UInt u[N];
+#if defined(CUZFP_PROBE) && CUZFP_PROBE == 2
+  {
+    const uint64_t base = rd.peek();
+    (void)budget;
+#pragma unroll
+    for (int i = 0; i < N; i++) u[i] = (UInt)(base >> (i & 31)) + (UInt)i;
+  }
+#elif defined(CUZFP_PROBE) && CUZFP_PROBE == 1
+  planes<UInt, DIMS> P;
+  {
+    const uint64_t base = rd.peek();
+    (void)budget;
+#pragma unroll
+    for (int k = 0; k < (int)sizeof(UInt) * 8; k++)
+      P.set(k, (typename plane_word<DIMS>::type)((base >> (k & 15)) ^ (uint64_t)k));
+  }
+  P.store(u);
+#else
   planes<UInt, DIMS> P;
   decode_planes<UInt, DIMS>(P, budget, maxprec, rd);
-  UInt u[N];
   P.store(u);
+#endif
   UInt q[N];
   constexpr UInt NB = nbmask<UInt>::value;
   permute_inv<DIMS>(u, q, NB, make_seq<N>());

@@ -24,7 +24,7 @@ TC = {np.dtype(np.int32): 1, np.dtype(np.int64): 2, np.dtype(np.float32): 3, np.
 def emu():
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
     if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(SRC), os.path.getmtime(HDR)):
-        subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wno-unknown-pragmas",
+        subprocess.check_call(["/opt/rocm/llvm/bin/clang++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wno-unknown-pragmas",
                                "-o", LIB, SRC])
     lib = ctypes.CDLL(LIB)
     args = [ctypes.c_int] + [ctypes.c_uint] * 3 + [ctypes.c_longlong] * 3 + [ctypes.c_uint]

@@ -55,6 +55,12 @@ for s in $STEPS; do
           python tools/kernel_probe.py ${PROBE_ARGS:-} > /dev/null 2>&1
         ok_or_stop $? counters_g$i
       done ;;
+    probe)
+      # phase costs: product kernels vs no plane coder vs no transpose (tools/probe.py)
+      timeout -k 10 600 python tools/probe.py run > "$OUT/probe_$TAG.log" 2>&1
+      ok_or_stop $? probe
+      timeout -k 10 600 python tools/probe.py run --field splitmix >> "$OUT/probe_$TAG.log" 2>&1
+      ok_or_stop $? probe_split; cat "$OUT/probe_$TAG.log" ;;
     *) echo "unknown step $s" ;;
   esac
 done
