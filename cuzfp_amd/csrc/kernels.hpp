@@ -117,6 +117,10 @@ struct LdsReader {
     next = wi + 3;
   }
   __device__ __forceinline__ uint64_t peek() const { return (w0 >> s) | ((w1 << 1) << (63 - s)); }
+  __device__ __forceinline__ void peek2(uint64_t& a, uint64_t& b) const {
+    a = (w0 >> s) | ((w1 << 1) << (63 - s));
+    b = (w1 >> s) | ((w2 << 1) << (63 - s));
+  }
   __device__ __forceinline__ void skip(unsigned n) {
     s += n;
     if (s >= 64) {

@@ -467,47 +467,97 @@ ZFP_HD void encode_planes(const planes<UInt, DIMS>& P, unsigned maxprec, Writer&
   }
 }
 
-// decode.c:288-321.  One 64-bit window per group: its bit 0 is the group test,
-// the trailing zeros after it are the run.  `bits` is the budget left; when it
-// ends inside a run the reference still deposits a one at the current
-// position (decode.c:311), and so does the min(z, lim) form below.  The group
-// step is branch-free (selects on the group bit), so a wave only pays for its
-// longest plane, not for per-lane if/else paths.
+// Decoder plane step (decode.c:288-321).
+//
+// Fast path, bit-parallel.  After the verbatim bits and a "1" group test the
+// plane's code is a sequence of segments  0^z 1 g  (zeros, the new one, the
+// group test after it: g = 1 means more ones follow) ending at the first g = 0.
+// So in the code c every run of ones starts at a segment's one and consists of
+// (one, g = 1) pairs -- except the last run, whose final one is followed by the
+// closing 0: the code ends at the first run of ODD length.  With
+//   F = the ones at even offsets inside their run      (the segments' ones)
+// the end is the lowest bit of F that is also the last bit of its run, and the
+// new plane ones are F's bits moved down past the g bits below them (the j-th
+// one of F by j).  Runs starting at even positions are found with one carrying
+// add (c + their start bits clears exactly those runs).
+//
+// The fast path applies when that whole code lies in the 64-bit window, inside
+// the budget, and ends below position N-1 (no implied one); otherwise -- a
+// dense plane, the block's last bits, or a one implied at N-1 -- the exact
+// sequential group loop below runs, whose trips follow the reference's
+// control flow bit for bit (including the one it deposits when the budget ends
+// inside a run, decode.c:311).
 template <int DIMS, typename PW, typename Reader>
 ZFP_HD PW decode_plane(unsigned& bits, unsigned& n, Reader& rd) {
   constexpr unsigned N = 1u << (2 * DIMS);
-  PW x = 0;
-  if (n) {
-    const unsigned m = umin(n, bits);
-    x = (PW)(rd.peek() & lowmask(m));
+  constexpr uint64_t EVEN = 0x5555555555555555ull;
+  uint64_t v0, v1;
+  rd.peek2(v0, v1);  // stream bits [pos, pos + 128)
+  const unsigned m = umin(n, bits);
+  PW x = (PW)(v0 & lowmask(m));
+  bits -= m;
+  if (!(n < N && bits)) {
     rd.skip(m);
-    bits -= m;
+    return x;
   }
-  if (n < N && bits) {
-    // leading group test: a "0" ends the plane at once, without a loop trip
-    const bool g0 = rd.peek() & 1;
-    rd.skip(1);
-    bits--;
-    bool more = g0;
-    // one trip per new one: the run of zeros, the one (unless implied at
-    // position N-1) and the following group test, all from one window
-    while (more) {
-      const uint64_t w = rd.peek();
-      const unsigned lim = umin(N - 1 - n, bits);   // zeros we may still read
-      const unsigned z = ctz64_or_64(w);            // zeros before the one
-      const bool found = z < lim;                   // the one is read, not implied
-      const unsigned adv = found ? z : lim;
-      n += adv;
-      x |= (PW)1 << n;
-      n++;
-      const unsigned used = adv + (found ? 1u : 0u);
-      // the group test after a read one: "1" = more ones follow
-      const bool gt = found && used < bits && n < N && ((w >> used) & 1);
-      const unsigned take = used + ((found && used < bits && n < N) ? 1u : 0u);
-      rd.skip(take);
-      bits -= take;
-      more = gt;  // with bits == 0 the next trip deposits at n (decode.c:311)
+  // m <= n < N <= 64 here, and m < 64: the window at the group test
+  const uint64_t win = (v0 >> m) | ((v1 << 1) << (63 - m));
+  if (!(win & 1)) {  // group test "0": no new ones in this plane
+    rd.skip(m + 1);
+    bits -= 1;
+    return x;
+  }
+  const uint64_t c = win >> 1;                   // 63 valid bits
+  const uint64_t starts = c & ~(c << 1);
+  const uint64_t erun = c & ~(c + (starts & EVEN));
+  const uint64_t F = (erun & EVEN) | (c & ~erun & ~EVEN);
+  const uint64_t oddend = F & ~(c >> 1);         // a pair's one with a 0 partner
+  const unsigned qe = ctz64_or_64(oddend);       // the last one of the code
+  const uint64_t Fm = F & lowmask(qe + 1);
+  const unsigned ones = (unsigned)__builtin_popcountll(Fm);
+  const unsigned plast = qe + 1 - ones;          // its plane offset from n
+  // code = "1" + c[0 .. qe+1]: qe + 3 bits, the closing 0 at c bit qe + 1 <= 62
+  const bool fast = qe <= 61 && qe + 3 <= bits && n + plast <= N - 2;
+  if (fast) {
+    uint64_t f = Fm;
+    PW y = 0;
+    unsigned j = 0;
+    while (f) {
+      const uint64_t low = f & (0 - f);
+      y |= (PW)(low >> j);
+      f ^= low;
+      j++;
     }
+    x |= y << n;
+    n += plast + 1;
+    rd.skip(m);
+    rd.skip(qe + 3);
+    bits -= qe + 3;
+    return x;
+  }
+  // exact sequential group loop, from just after the "1" group test
+  rd.skip(m);
+  rd.skip(1);
+  bits -= 1;
+  bool more = true;
+  // one trip per new one: the run of zeros, the one (unless implied at
+  // position N-1) and the following group test, all from one window
+  while (more) {
+    const uint64_t w = rd.peek();
+    const unsigned lim = umin(N - 1 - n, bits);   // zeros we may still read
+    const unsigned z = ctz64_or_64(w);            // zeros before the one
+    const bool found = z < lim;                   // the one is read, not implied
+    const unsigned adv = found ? z : lim;
+    n += adv;
+    x |= (PW)1 << n;
+    n++;
+    const unsigned used = adv + (found ? 1u : 0u);
+    // the group test after a read one: "1" = more ones follow
+    const bool gt = found && used < bits && n < N && ((w >> used) & 1);
+    const unsigned take = used + ((found && used < bits && n < N) ? 1u : 0u);
+    rd.skip(take);
+    bits -= take;
+    more = gt;  // with bits == 0 the next trip deposits at n (decode.c:311)
   }
   return x;
 }

@@ -48,6 +48,12 @@ struct HostReader {
     const size_t w = pos >> 6;
     return sh ? (word(w) >> sh) | (word(w + 1) << (64 - sh)) : word(w);
   }
+  void peek2(uint64_t& a, uint64_t& b) {
+    a = peek();
+    pos += 64;
+    b = peek();
+    pos -= 64;
+  }
   void skip(unsigned n) { pos += n; }
 };
 

@@ -55,6 +55,13 @@ for s in $STEPS; do
           python tools/kernel_probe.py ${PROBE_ARGS:-} > /dev/null 2>&1
         ok_or_stop $? counters_g$i
       done ;;
+    sizes)
+      # throughput vs problem size (rounds of resident waves): 128^3 .. 512^3
+      for sz in 128 192 256 384 512; do
+        timeout -k 10 300 python bench.py --size $sz --steps 20 --warmup 5 --no-cpu-baseline --no-host-path > "$OUT/bench_size${sz}_$TAG.json" 2>&1
+        ok_or_stop $? size$sz
+        python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print($sz, d['value'], d['encode_ms'], d['decode_ms'])" "$OUT/bench_size${sz}_$TAG.json"
+      done ;;
     probe)
       # phase costs: product kernels vs no plane coder vs no transpose (tools/probe.py)
       timeout -k 10 600 python tools/probe.py run > "$OUT/probe_$TAG.log" 2>&1
