@@ -21,6 +21,28 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#if defined(CUZFP_PROBE) && CUZFP_PROBE == 9
+// Diagnostic build (tools/probe.py stamps): lane 0 of every wave records
+// s_memtime at the codec's phase boundaries, plus its HW_ID / XCC_ID.
+#define CUZFP_STAMP_WAVES 65536
+__device__ uint64_t g_stamps[CUZFP_STAMP_WAVES * 8];
+#define ZFP_STAMP(i)                                                              \
+  do {                                                                            \
+    if (threadIdx.x == 0 && blockIdx.x < CUZFP_STAMP_WAVES)                      \
+      g_stamps[blockIdx.x * 8 + 1 + (i)] = __builtin_amdgcn_s_memtime();         \
+  } while (0)
+__device__ __forceinline__ void stamp_hwid() {
+  uint32_t hw, xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  if (threadIdx.x == 0 && blockIdx.x < CUZFP_STAMP_WAVES)
+    g_stamps[blockIdx.x * 8] = (uint64_t)hw | ((uint64_t)xcc << 32);
+}
+#define ZFP_STAMP_HWID() stamp_hwid()
+#else
+#define ZFP_STAMP_HWID()
+#endif
+
 #include "zfp_block.hpp"
 #include "launch.hpp"
 
@@ -30,8 +52,9 @@ namespace cuzfp {
 // LDS bit writers / reader (one lane, one block)
 
 // maxbits % 64 == 0: the lane owns whole words [lane*W, lane*W + W).  Full
-// 64-bit words are flushed to LDS; once W words are out the block is full, so
-// bits the coder produced past maxbits stay in `acc` and are dropped.
+// 64-bit words are flushed to LDS; once W words are out the block is full, and
+// whatever the coder still produces (it finishes the plane it is in) is
+// dropped.
 struct LdsWordWriter {
   uint64_t* p;
   uint32_t words, w, cnt;
@@ -41,7 +64,8 @@ struct LdsWordWriter {
     acc |= v << cnt;
     const unsigned c = cnt + n;
     if (c >= 64) {
-      p[w++] = acc;
+      if (w < words) p[w] = acc;     // bits past maxbits are dropped
+      w++;
       acc = (v >> 1) >> (63 - cnt);  // the bits of v that did not fit (0 if cnt == 0)
       cnt = c - 64;
     } else {
@@ -50,7 +74,8 @@ struct LdsWordWriter {
   }
   __device__ __forceinline__ void zero_bit() {
     if (++cnt == 64) {
-      p[w++] = acc;
+      if (w < words) p[w] = acc;
+      w++;
       acc = 0;
       cnt = 0;
     }
@@ -72,6 +97,7 @@ struct LdsBitWriter {
   uint64_t acc;
   __device__ __forceinline__ bool full() const { return pos + cnt >= end; }
   __device__ __forceinline__ void emit(uint64_t v) {
+    if (pos >= end) return;  // bits past maxbits are dropped
     const uint32_t room = end - pos;
     if (room < 64) v &= lowmask(room);
     const uint32_t w = pos >> 6, sh = pos & 63;
@@ -254,6 +280,8 @@ __global__ __launch_bounds__(kLanes, 4) void zfp_encode(const Scalar* __restrict
   const uint32_t wave = g.wave0 + blockIdx.x;
   const uint32_t lane = threadIdx.x;
   const uint32_t b = wave * kLanes + lane;
+  ZFP_STAMP_HWID();
+  ZFP_STAMP(0);
   if constexpr (!ALIGNED) {
     for (uint32_t j = lane; j < g.maxbits + 2; j += kLanes) lds[j] = 0;
     __syncthreads();
@@ -282,6 +310,7 @@ __global__ __launch_bounds__(kLanes, 4) void zfp_encode(const Scalar* __restrict
   } else {
     for (uint32_t j = lane; j < nwords; j += kLanes) out[j] = lds[j];
   }
+  ZFP_STAMP(6);
 }
 
 template <typename Scalar, int DIMS, bool FAST>
@@ -302,8 +331,11 @@ __global__ __launch_bounds__(kLanes, 4) void zfp_decode(const uint64_t* __restri
   } else {
     for (uint32_t j = lane; j < nwords; j += kLanes) lds[j] = in[j];
   }
+  ZFP_STAMP_HWID();
+  ZFP_STAMP(0);
   if (lane < 3) lds[nwords + lane] = 0;  // reader look-ahead slack
   __syncthreads();
+  ZFP_STAMP(5);
   if (b < g.nblocks) {
     LdsReader rd;
     rd.lds = lds;
@@ -312,6 +344,7 @@ __global__ __launch_bounds__(kLanes, 4) void zfp_decode(const uint64_t* __restri
     decode_block<Scalar, DIMS>(f, g.maxbits, rd);
     scatter<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
   }
+  ZFP_STAMP(6);
 }
 
 // ---------------------------------------------------------------------------

@@ -35,6 +35,11 @@
 #define ZFP_HD inline
 #endif
 
+// Diagnostic phase stamps (tools/probe.py, CUZFP_PROBE == 9 builds only).
+#ifndef ZFP_STAMP
+#define ZFP_STAMP(i)
+#endif
+
 namespace cuzfp {
 
 // ---------------------------------------------------------------------------
@@ -378,59 +383,55 @@ ZFP_HD unsigned ctz64_or_64(uint64_t x) {
 // code is: its first n bits verbatim, then for every further one bit at
 // position p a group "1" + the zeros before p + that one (implied, so omitted,
 // when p = N-1), then a closing "0" group test if positions remain.  The
-// writer is never asked to clip: it reports full() once the block's maxbits
-// are written and the plane loop stops there, so the stream is exactly the
-// reference's budget-truncated prefix.
+// common case is two writer calls and no branch on the data: the verbatim bits,
+// then the whole group code G built with one shift per new one.  Writers drop
+// bits past maxbits, so a plane that crosses the budget needs no clipping here
+// and the stream is exactly the reference's budget-truncated prefix; the plane
+// loop stops once the writer reports full().
 template <int DIMS, typename PW, typename Writer>
 ZFP_HD void encode_plane(PW x, unsigned& n, Writer& wr) {
   constexpr unsigned N = 1u << (2 * DIMS);
-  // verbatim part
-  if (n) wr.put(x & (PW)lowmask(n), n);
+  wr.put(x & (PW)lowmask(n), n);  // verbatim part (nothing when n = 0)
   // new ones, in the frame of the first not-yet-significant coefficient
   const PW r = n < N ? (PW)(x >> n) : (PW)0;
-  if (!r) {
-    if (n < N && !wr.full()) wr.zero_bit();  // group test "0"
-  } else if (!wr.full()) {
-    // With t new ones at relative positions p_0 < ... < p_{t-1} the group
-    // code is  1 (z_0 zeros) 1 1 (z_1 zeros) 1 1 ... (z_{t-1} zeros) 1 0,
-    // i.e. "1" followed by the segment up to p_{t-1} with every one doubled,
-    // the last one's partner being the closing "0" -- or, when the last one
-    // sits at position N-1, both its bit and the closing test omitted.  The
-    // j-th one therefore lands at bit p_j + j + 1 (and its partner at + 2):
-    // F collects those positions with one shift per one, no branches on the
-    // stream.
-    const unsigned pt = (unsigned)(8 * sizeof(PW) - 1) - (unsigned)(sizeof(PW) == 8 ? __builtin_clzll((uint64_t)r) : __builtin_clz((uint32_t)r));
-    const unsigned t = (unsigned)(sizeof(PW) == 8 ? __builtin_popcountll((uint64_t)r) : __builtin_popcount((uint32_t)r));
-    const unsigned qmax = pt + t - 1;  // F position of the last one
-    const bool last_n = pt + n == N - 1;
-    if (qmax <= 61) {
-      uint64_t F = 0;
-      PW rr = r;
-      unsigned j = 0;
-      while (rr) {
-        const PW low = rr & (PW)(0 - rr);
-        F |= (uint64_t)low << j;
-        rr ^= low;
-        j++;
-      }
-      const unsigned L = qmax + (last_n ? 1u : 3u);
-      const uint64_t G = (1ull | (F << 1) | (F << 2)) & lowmask(last_n ? L : L - 1);
-      wr.put(G, L);
-      n += pt + 1;
-    } else {
-      // dense plane (many ones early in a wide block): one put per group
-      PW rest = r;
-      unsigned base = n;
-      while (rest && !wr.full()) {
-        const unsigned p = ctz(rest);
-        const bool last = base + p == N - 1;
-        const unsigned z = p - (n - base);
-        wr.put(last ? 1ull : (1ull | (2ull << z)), z + (last ? 1u : 2u));
-        n = base + p + 1;
-        rest &= rest - 1;
-      }
-      if (n < N && !wr.full()) wr.zero_bit();
+  // With t new ones at relative positions p_0 < ... < p_{t-1} the group code
+  // is  1 (z_0 zeros) 1 1 (z_1 zeros) 1 1 ... (z_{t-1} zeros) 1 0,  i.e. "1"
+  // followed by the segment up to p_{t-1} with every one doubled, the last
+  // one's partner being the closing "0" -- or, when the last one sits at
+  // position N-1, both its bit and the closing test omitted.  The j-th one
+  // therefore lands at bit p_j + j + 1 (and its partner at + 2).  No new ones:
+  // the single group test "0" (none at all once n = N).
+  const unsigned t = (unsigned)(sizeof(PW) == 8 ? __builtin_popcountll((uint64_t)r) : __builtin_popcount((uint32_t)r));
+  const unsigned pt = r ? (unsigned)(8 * sizeof(PW) - 1) - (unsigned)(sizeof(PW) == 8 ? __builtin_clzll((uint64_t)r) : __builtin_clz((uint32_t)r)) : 0u;
+  const unsigned qmax = pt + t - 1;  // G position of the last one, minus 1
+  if (!r || qmax <= 61) {
+    uint64_t F = 0;
+    PW rr = r;
+    unsigned j = 0;
+    while (rr) {
+      const PW low = rr & (PW)(0 - rr);
+      F |= (uint64_t)low << j;
+      rr ^= low;
+      j++;
     }
+    const bool last_n = pt + n == N - 1;
+    const unsigned L = r ? qmax + (last_n ? 1u : 3u) : (n < N ? 1u : 0u);
+    const uint64_t G = r ? (1ull | (F << 1) | (F << 2)) & lowmask(last_n ? L : L - 1) : 0ull;
+    wr.put(G, L);
+    n += r ? pt + 1 : 0u;
+  } else {
+    // dense plane (many ones early in a wide block): one put per group
+    PW rest = r;
+    unsigned base = n;
+    while (rest && !wr.full()) {
+      const unsigned p = ctz(rest);
+      const bool last = base + p == N - 1;
+      const unsigned z = p - (n - base);
+      wr.put(last ? 1ull : (1ull | (2ull << z)), z + (last ? 1u : 2u));
+      n = base + p + 1;
+      rest &= rest - 1;
+    }
+    if (n < N && !wr.full()) wr.zero_bit();
   }
 }
 
@@ -661,6 +662,7 @@ ZFP_HD void encode_block(const Scalar* f, unsigned maxbits, Writer& wr) {
   if constexpr (!T::is_int) {
     // encode.c:187-216
     const int emax = fp<Scalar>::template emax<N>((const Scalar*)f);
+    ZFP_STAMP(1);
     maxprec = precision<DIMS>(emax, T::prec);
     const unsigned e = maxprec ? (unsigned)(emax + T::ebias) : 0u;
     if (!e) {  // all-zero block: a single 0 bit, then padding
@@ -714,7 +716,8 @@ ZFP_HD void encode_block(const Scalar* f, unsigned maxbits, Writer& wr) {
   UInt u[N];
   constexpr UInt NB = nbmask<UInt>::value;
   permute_fwd<DIMS>(q, u, NB, make_seq<N>());
-#if defined(CUZFP_PROBE) && CUZFP_PROBE > 0
+  ZFP_STAMP(2);
+#if defined(CUZFP_PROBE) && (CUZFP_PROBE == 1 || CUZFP_PROBE == 2)
   // timing probes (tools/probe.py; never built into the product library):
   // 1 = no plane coder, 2 = no transpose either
   uint64_t acc = 0;
@@ -732,7 +735,9 @@ ZFP_HD void encode_block(const Scalar* f, unsigned maxbits, Writer& wr) {
 #else
   planes<UInt, DIMS> P;
   P.load(u);
+  ZFP_STAMP(3);
   encode_planes<UInt, DIMS>(P, maxprec, wr);
+  ZFP_STAMP(4);
 #endif
   wr.finish();
 }
@@ -779,12 +784,15 @@ ZFP_HD void decode_block(Scalar* f, unsigned maxbits, Reader& rd) {
 #else
   planes<UInt, DIMS> P;
   decode_planes<UInt, DIMS>(P, budget, maxprec, rd);
+  ZFP_STAMP(1);
   P.store(u);
+  ZFP_STAMP(2);
 #endif
   UInt q[N];
   constexpr UInt NB = nbmask<UInt>::value;
   permute_inv<DIMS>(u, q, NB, make_seq<N>());
   inv_xform<DIMS>(q);
+  ZFP_STAMP(3);
   if constexpr (!T::is_int) {
     const Scalar s = (Scalar)fp<Scalar>::pow2(emax - (T::prec - 2));
 #pragma unroll

@@ -24,6 +24,7 @@ struct HostWriter {
   size_t pos, end;
   bool full() const { return pos >= end; }
   void put(uint64_t v, unsigned n) {
+    if (pos >= end) return;
     if (pos + n > end) {
       n = (unsigned)(end - pos);
       v &= cuzfp::lowmask(n);
@@ -34,7 +35,9 @@ struct HostWriter {
     if (sh + n > 64) s[(pos >> 6) + 1] |= v >> (64 - sh);
     pos += n;
   }
-  void zero_bit() { pos++; }
+  void zero_bit() {
+    if (pos < end) pos++;
+  }
   void finish() {}
 };
 

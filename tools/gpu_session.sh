@@ -62,6 +62,14 @@ for s in $STEPS; do
         ok_or_stop $? size$sz
         python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print($sz, d['value'], d['encode_ms'], d['decode_ms'])" "$OUT/bench_size${sz}_$TAG.json"
       done ;;
+    stamps)
+      # per-wave phase timestamps (s_memtime) of the diagnostic build
+      timeout -k 10 300 python tools/probe.py stamps > "$OUT/stamps_$TAG.log" 2>&1
+      ok_or_stop $? stamps
+      timeout -k 10 300 python tools/probe.py stamps --field splitmix >> "$OUT/stamps_$TAG.log" 2>&1
+      ok_or_stop $? stamps_split
+      timeout -k 10 300 python tools/probe.py stamps --size 512 >> "$OUT/stamps_$TAG.log" 2>&1
+      ok_or_stop $? stamps_512; cat "$OUT/stamps_$TAG.log" ;;
     probe)
       # phase costs: product kernels vs no plane coder vs no transpose (tools/probe.py)
       timeout -k 10 600 python tools/probe.py run > "$OUT/probe_$TAG.log" 2>&1

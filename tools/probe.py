@@ -18,10 +18,13 @@ sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "build", "probe")
 
 
+VARIANTS = (0, 1, 2, 9)
+
+
 def build():
     from cuzfp_amd import build as b
     procs = []
-    for v in (0, 1, 2):
+    for v in VARIANTS:
         d = os.path.join(OUT, f"p{v}")
         os.makedirs(d, exist_ok=True)
         objs = []
@@ -31,7 +34,7 @@ def build():
             procs.append(subprocess.Popen([b.HIPCC, *b.CXXFLAGS, f"-DCUZFP_PROBE={v}", "-c",
                                            os.path.join(b.CSRC, u + ".hip"), "-o", o]))
     assert all(p.wait() == 0 for p in procs)
-    for v in (0, 1, 2):
+    for v in VARIANTS:
         d = os.path.join(OUT, f"p{v}")
         objs = [os.path.join(d, u + ".o") for u in ("inst_f32", "inst_f64", "inst_i32", "inst_i64", "capi")]
         subprocess.check_call([b.HIPCC, f"--offload-arch={b.ARCH}", "-shared", "-fPIC", "-o",
@@ -71,6 +74,71 @@ print(json.dumps(dict(enc_us=t(lambda: cz.encode(x, mb, out=w)), dec_us=t(lambda
         print(f"p{v}", res[f"p{v}"], flush=True)
 
 
+STAMP_CODE = r"""
+import os, sys, json, ctypes, torch, numpy as np
+sys.path.insert(0, @ROOT@)
+os.environ['CUZFP_HIP_LIB'] = @LIB@
+import cuzfp_amd as cz
+from cuzfp_amd.datagen import polynomial_field, splitmix_uniform
+shape = (@SIZE@,)*3
+arr = polynomial_field(shape) if @FIELD@ == 'polynomial' else splitmix_uniform(shape)
+x = torch.from_numpy(arr).cuda()
+mb = cz.rate_to_maxbits(8, arr.dtype, 3)
+lib = cz.library()
+w = cz.encode(x, mb); y = cz.decode(w, shape, x.dtype, mb)
+nw = (@SIZE@ // 4) ** 3 // 64
+out = {}
+for name, fn in (("encode", lambda: cz.encode(x, mb, out=w)), ("decode", lambda: cz.decode(w, shape, x.dtype, mb, out=y))):
+    for _ in range(3): fn()
+    torch.cuda.synchronize()
+    lib.cuzfp_hip_probe_clear()
+    fn(); torch.cuda.synchronize()
+    buf = np.zeros(65536 * 8, np.uint64)
+    lib.cuzfp_hip_probe_stamps(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes))
+    np.save(os.path.join(@OUTDIR@, "stamps_" + name + "_" + @FIELD@ + "_" + str(@SIZE@) + ".npy"), buf.reshape(-1, 8)[:nw])
+print("ok")
+"""
+
+
+def stamps(size, field, outdir):
+    lib = os.path.join(OUT, "p9", "libcuzfp_hip.so")
+    code = STAMP_CODE.replace("@ROOT@", repr(ROOT)).replace("@LIB@", repr(lib)).replace("@SIZE@", str(size)) \
+        .replace("@FIELD@", repr(field)).replace("@OUTDIR@", repr(outdir))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    if r.returncode:
+        print(r.stderr[-3000:])
+        raise SystemExit(r.returncode)
+    for name in ("encode", "decode"):
+        analyse(os.path.join(outdir, f"stamps_{name}_{field}_{size}.npy"), name)
+
+
+def analyse(path, name):
+    import numpy as np
+    a = np.load(path).astype(np.int64)
+    hw, t = a[:, 0], a[:, 1:]
+    t0 = t[:, 0].min()
+    rel = t - t0
+    end = rel[:, 6] if name == "encode" else rel[:, 6]
+    print(f"== {name}: {len(a)} waves, span {end.max()} cycles")
+    labels = (["start", "emax(load)", "transform", "transpose", "planes", "-", "end"] if name == "encode"
+              else ["start", "planes", "transpose", "inv-xform", "-", "copy-in", "end"])
+    order = [0, 1, 2, 3, 4, 6] if name == "encode" else [0, 5, 1, 2, 3, 6]
+    prev = None
+    for k in order:
+        col = rel[:, k]
+        line = f"  {labels[k]:11s} at: min {col.min():7d} p50 {int(np.median(col)):7d} max {col.max():7d}"
+        if prev is not None:
+            d = rel[:, k] - rel[:, prev]
+            line += f"   phase: mean {int(d.mean()):6d} p50 {int(np.median(d)):6d} max {d.max():6d}"
+        print(line)
+        prev = k
+    simd = ((hw >> 32) << 16) | (((hw >> 13) & 3) << 12) | (((hw >> 12) & 1) << 11) | (((hw >> 8) & 15) << 4) | ((hw >> 4) & 3)
+    u, cnt = np.unique(simd, return_counts=True)
+    print(f"  distinct SIMDs {len(u)}, waves per SIMD: min {cnt.min()} max {cnt.max()} mean {cnt.mean():.2f}")
+    life = rel[:, 6] - rel[:, 0]
+    print(f"  wave lifetime: mean {int(life.mean())} p50 {int(np.median(life))} max {life.max()}")
+
+
 if __name__ == "__main__":
     import argparse
     ap = argparse.ArgumentParser()
@@ -80,5 +148,9 @@ if __name__ == "__main__":
     a = ap.parse_args()
     if a.cmd == "build":
         build()
+    elif a.cmd == "stamps":
+        od = os.path.join(ROOT, "gpurun_out")
+        os.makedirs(od, exist_ok=True)
+        stamps(a.size, a.field, od)
     else:
         run(a.size, a.field)
