@@ -51,39 +51,30 @@ namespace cuzfp {
 // ---------------------------------------------------------------------------
 // LDS bit writers / reader (one lane, one block)
 
-// maxbits % 64 == 0: the lane owns whole words [lane*W, lane*W + W).  Full
-// 64-bit words are flushed to LDS; once W words are out the block is full, and
-// whatever the coder still produces (it finishes the plane it is in) is
-// dropped.
+// maxbits % 64 == 0: the lane owns whole words [lane*W, lane*W + W).  Every
+// put stores the word being filled (so a flushed word lands in LDS without a
+// branch on the flush); once W words are done the block is full, and stores of
+// whatever the coder still produces (it finishes the plane it is in) go to the
+// lane's private dummy word instead.
 struct LdsWordWriter {
-  uint64_t* p;
-  uint32_t words, w, cnt;
-  uint64_t acc;
-  __device__ __forceinline__ bool full() const { return w >= words; }
+  uint64_t* p;      // the lane's W words
+  uint64_t* dummy;  // a private LDS word past the wave's segment
+  uint32_t words, pos;  // pos: bits produced so far
+  uint64_t acc;         // bits [64*(pos/64), pos)
+  __device__ __forceinline__ bool full() const { return pos >= 64 * words; }
   __device__ __forceinline__ void put(uint64_t v, unsigned n) {
+    const uint32_t cnt = pos & 63, w = pos >> 6;
     acc |= v << cnt;
-    const unsigned c = cnt + n;
-    if (c >= 64) {
-      if (w < words) p[w] = acc;     // bits past maxbits are dropped
-      w++;
-      acc = (v >> 1) >> (63 - cnt);  // the bits of v that did not fit (0 if cnt == 0)
-      cnt = c - 64;
-    } else {
-      cnt = c;
-    }
+    uint64_t* dst = w < words ? p + w : dummy;
+    *dst = acc;
+    acc = cnt + n >= 64 ? (v >> 1) >> (63 - cnt) : acc;  // the bits of v that did not fit
+    pos += n;
   }
-  __device__ __forceinline__ void zero_bit() {
-    if (++cnt == 64) {
-      if (w < words) p[w] = acc;
-      w++;
-      acc = 0;
-      cnt = 0;
-    }
-  }
+  __device__ __forceinline__ void zero_bit() { put(0, 1); }
   __device__ __forceinline__ void finish() {
-    if (w < words) {
-      p[w++] = acc;
-      while (w < words) p[w++] = 0;
+    for (uint32_t w = pos >> 6; w < words; w++) {
+      p[w] = acc;
+      acc = 0;
     }
   }
 };
@@ -128,33 +119,49 @@ struct LdsBitWriter {
   }
 };
 
-// 128-bit window over the wave's LDS stream image, plus one word prefetched,
-// so a refill never waits on the LDS read it issues.
+// Window over the wave's LDS stream image: w0..w5 = words base .. base+5, the
+// reading position at bit s of w0; peek()/peek2() use w0..w2.  skip() (up to
+// 128 bits, i.e. a whole plane at once) is branch-free: it shifts the window
+// by 0, 1 or 2 words and re-reads words base+4 and base+5 -- reads whose values
+// are first needed at the NEXT skip, so they never stall the lane.
 struct LdsReader {
   const uint64_t* lds;
-  uint64_t w0, w1, w2;
-  uint32_t s, next;
+  uint64_t w0, w1, w2, w3, w4, w5;
+  uint32_t s, base;
   __device__ __forceinline__ void init(uint32_t bitpos) {
-    const uint32_t wi = bitpos >> 6;
+    base = bitpos >> 6;
     s = bitpos & 63;
-    w0 = lds[wi];
-    w1 = lds[wi + 1];
-    w2 = lds[wi + 2];
-    next = wi + 3;
+    w0 = lds[base];
+    w1 = lds[base + 1];
+    w2 = lds[base + 2];
+    w3 = lds[base + 3];
+    w4 = lds[base + 4];
+    w5 = lds[base + 5];
   }
   __device__ __forceinline__ uint64_t peek() const { return (w0 >> s) | ((w1 << 1) << (63 - s)); }
   __device__ __forceinline__ void peek2(uint64_t& a, uint64_t& b) const {
     a = (w0 >> s) | ((w1 << 1) << (63 - s));
     b = (w1 >> s) | ((w2 << 1) << (63 - s));
   }
-  __device__ __forceinline__ void skip(unsigned n) {
+  __device__ __forceinline__ void skip(unsigned n) {  // n <= 128
     s += n;
-    if (s >= 64) {
-      s -= 64;
-      w0 = w1;
-      w1 = w2;
-      w2 = lds[next++];
-    }
+    const uint32_t adv = s >> 6;
+    s &= 63;
+    // two one-word steps (a nested select would be turned into a
+    // runtime-indexed window in scratch memory)
+    const bool a1 = adv != 0, a2 = adv > 1;
+    w0 = a1 ? w1 : w0;
+    w1 = a1 ? w2 : w1;
+    w2 = a1 ? w3 : w2;
+    w3 = a1 ? w4 : w3;
+    w4 = a1 ? w5 : w4;
+    w0 = a2 ? w1 : w0;
+    w1 = a2 ? w2 : w1;
+    w2 = a2 ? w3 : w2;
+    w3 = a2 ? w4 : w3;
+    base += adv;
+    w4 = lds[base + 4];
+    w5 = lds[base + 5];
   }
 };
 
@@ -291,7 +298,7 @@ __global__ __launch_bounds__(kLanes, 4) void zfp_encode(const Scalar* __restrict
     gather<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
     if constexpr (ALIGNED) {
       const uint32_t W = g.maxbits >> 6;
-      LdsWordWriter wr{lds + lane * W, W, 0, 0, 0};
+      LdsWordWriter wr{lds + lane * W, lds + (size_t)kLanes * W + lane, W, 0, 0};
       encode_block<Scalar, DIMS>(f, g.maxbits, wr);
     } else {
       LdsBitWriter wr{lds, lane * g.maxbits, (lane + 1) * g.maxbits, 0, 0};
@@ -333,7 +340,7 @@ __global__ __launch_bounds__(kLanes, 4) void zfp_decode(const uint64_t* __restri
   }
   ZFP_STAMP_HWID();
   ZFP_STAMP(0);
-  if (lane < 3) lds[nwords + lane] = 0;  // reader look-ahead slack
+  if (lane < 6) lds[nwords + lane] = 0;  // reader look-ahead slack
   __syncthreads();
   ZFP_STAMP(5);
   if (b < g.nblocks) {
@@ -356,7 +363,7 @@ int launch_encode_t(const void* data, const Geometry& g, bool fast, uint64_t* st
   Geometry gg = g;
   gg.wave0 = wave0;
   gg.vec_io = (g.maxbits % 2 == 0) && ((uintptr_t)stream % 16 == 0);
-  const size_t lds = ((size_t)g.maxbits + 2) * 8;
+  const size_t lds = ((size_t)g.maxbits + kLanes) * 8;  // + the writers' dummy words
   const bool aligned = (g.maxbits & 63) == 0;
   const Scalar* d = (const Scalar*)data;
   if (fast && aligned)
@@ -378,7 +385,7 @@ int launch_decode_t(const uint64_t* stream, const Geometry& g, bool fast, void* 
   Geometry gg = g;
   gg.wave0 = wave0;
   gg.vec_io = (g.maxbits % 2 == 0) && ((uintptr_t)stream % 16 == 0);
-  const size_t lds = ((size_t)g.maxbits + 3) * 8;
+  const size_t lds = ((size_t)g.maxbits + 6) * 8;
   Scalar* d = (Scalar*)data;
   if (fast)
     hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, true>), dim3(nwaves), dim3(kLanes), lds, st, stream, gg, d);

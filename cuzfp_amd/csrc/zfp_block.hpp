@@ -393,7 +393,7 @@ ZFP_HD void encode_plane(PW x, unsigned& n, Writer& wr) {
   constexpr unsigned N = 1u << (2 * DIMS);
   wr.put(x & (PW)lowmask(n), n);  // verbatim part (nothing when n = 0)
   // new ones, in the frame of the first not-yet-significant coefficient
-  const PW r = n < N ? (PW)(x >> n) : (PW)0;
+  const PW r = n < N ? (PW)(x >> (n & (8 * sizeof(PW) - 1))) : (PW)0;
   // With t new ones at relative positions p_0 < ... < p_{t-1} the group code
   // is  1 (z_0 zeros) 1 1 (z_1 zeros) 1 1 ... (z_{t-1} zeros) 1 0,  i.e. "1"
   // followed by the segment up to p_{t-1} with every one doubled, the last
@@ -404,7 +404,7 @@ ZFP_HD void encode_plane(PW x, unsigned& n, Writer& wr) {
   const unsigned t = (unsigned)(sizeof(PW) == 8 ? __builtin_popcountll((uint64_t)r) : __builtin_popcount((uint32_t)r));
   const unsigned pt = r ? (unsigned)(8 * sizeof(PW) - 1) - (unsigned)(sizeof(PW) == 8 ? __builtin_clzll((uint64_t)r) : __builtin_clz((uint32_t)r)) : 0u;
   const unsigned qmax = pt + t - 1;  // G position of the last one, minus 1
-  if (!r || qmax <= 61) {
+  if (__builtin_expect(!r || qmax <= 61, 1)) {
     uint64_t F = 0;
     PW rr = r;
     unsigned j = 0;
@@ -497,17 +497,14 @@ ZFP_HD PW decode_plane(unsigned& bits, unsigned& n, Reader& rd) {
   const unsigned m = umin(n, bits);
   PW x = (PW)(v0 & lowmask(m));
   bits -= m;
-  if (!(n < N && bits)) {
-    rd.skip(m);
-    return x;
-  }
-  // m <= n < N <= 64 here, and m < 64: the window at the group test
-  const uint64_t win = (v0 >> m) | ((v1 << 1) << (63 - m));
-  if (!(win & 1)) {  // group test "0": no new ones in this plane
-    rd.skip(m + 1);
-    bits -= 1;
-    return x;
-  }
+  // The group part exists while positions and budget remain; then m <= n < N
+  // <= 64 and m < 64, and `win` is the window at the leading group test.  All
+  // of it is computed for every lane and selected, so the wave does not branch
+  // on the data (a lane without group part, or with a "0" group test, gets an
+  // empty F and consumes 0 or 1 bit).
+  const bool grp = n < N && bits;
+  const uint64_t win = (v0 >> (m & 63)) | ((v1 << 1) << (63 - (m & 63)));
+  const bool g0 = grp && (win & 1);
   const uint64_t c = win >> 1;                   // 63 valid bits
   const uint64_t starts = c & ~(c << 1);
   const uint64_t erun = c & ~(c + (starts & EVEN));
@@ -519,8 +516,8 @@ ZFP_HD PW decode_plane(unsigned& bits, unsigned& n, Reader& rd) {
   const unsigned plast = qe + 1 - ones;          // its plane offset from n
   // code = "1" + c[0 .. qe+1]: qe + 3 bits, the closing 0 at c bit qe + 1 <= 62
   const bool fast = qe <= 61 && qe + 3 <= bits && n + plast <= N - 2;
-  if (fast) {
-    uint64_t f = Fm;
+  if (__builtin_expect(!g0 || fast, 1)) {
+    uint64_t f = g0 ? Fm : 0ull;
     PW y = 0;
     unsigned j = 0;
     while (f) {
@@ -529,11 +526,11 @@ ZFP_HD PW decode_plane(unsigned& bits, unsigned& n, Reader& rd) {
       f ^= low;
       j++;
     }
-    x |= y << n;
-    n += plast + 1;
-    rd.skip(m);
-    rd.skip(qe + 3);
-    bits -= qe + 3;
+    x |= y << (n & (8 * sizeof(PW) - 1));
+    const unsigned used = g0 ? qe + 3 : (grp ? 1u : 0u);
+    n += g0 ? plast + 1 : 0u;
+    rd.skip(m + used);
+    bits -= used;
     return x;
   }
   // exact sequential group loop, from just after the "1" group test
