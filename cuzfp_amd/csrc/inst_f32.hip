@@ -14,7 +14,7 @@ extern "C" int cuzfp_hip_probe_stamps(void* dst, size_t bytes) {
   return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_stamps), bytes, 0, hipMemcpyDeviceToHost);
 }
 extern "C" int cuzfp_hip_probe_clear() {
-  static uint64_t zero[CUZFP_STAMP_WAVES * 8];
+  static uint64_t zero[CUZFP_STAMP_WAVES * 10];
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
 }
 #endif

@@ -25,22 +25,29 @@
 // Diagnostic build (tools/probe.py stamps): lane 0 of every wave records
 // s_memtime at the codec's phase boundaries, plus its HW_ID / XCC_ID.
 #define CUZFP_STAMP_WAVES 65536
-__device__ uint64_t g_stamps[CUZFP_STAMP_WAVES * 8];
+__device__ uint64_t g_stamps[CUZFP_STAMP_WAVES * 10];
 #define ZFP_STAMP(i)                                                              \
   do {                                                                            \
     if (threadIdx.x == 0 && blockIdx.x < CUZFP_STAMP_WAVES)                      \
-      g_stamps[blockIdx.x * 8 + 1 + (i)] = __builtin_amdgcn_s_memtime();         \
+      g_stamps[blockIdx.x * 10 + 1 + (i)] = __builtin_amdgcn_s_memtime();        \
   } while (0)
 __device__ __forceinline__ void stamp_hwid() {
   uint32_t hw, xcc;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
   if (threadIdx.x == 0 && blockIdx.x < CUZFP_STAMP_WAVES)
-    g_stamps[blockIdx.x * 8] = (uint64_t)hw | ((uint64_t)xcc << 32);
+    g_stamps[blockIdx.x * 10] = (uint64_t)hw | ((uint64_t)xcc << 32);
 }
+// global 100 MHz clock, comparable across CUs: slot 8 = start, 9 = end
+__device__ __forceinline__ void stamp_real(int slot) {
+  if (threadIdx.x == 0 && blockIdx.x < CUZFP_STAMP_WAVES)
+    g_stamps[blockIdx.x * 10 + slot] = __builtin_amdgcn_s_memrealtime();
+}
+#define ZFP_STAMP_REAL(slot) stamp_real(slot)
 #define ZFP_STAMP_HWID() stamp_hwid()
 #else
 #define ZFP_STAMP_HWID()
+#define ZFP_STAMP_REAL(slot)
 #endif
 
 #include "zfp_block.hpp"
@@ -51,32 +58,27 @@ namespace cuzfp {
 // ---------------------------------------------------------------------------
 // LDS bit writers / reader (one lane, one block)
 
-// maxbits % 64 == 0: the lane owns whole words [lane*W, lane*W + W).  Every
-// put stores the word being filled (so a flushed word lands in LDS without a
-// branch on the flush); once W words are done the block is full, and stores of
-// whatever the coder still produces (it finishes the plane it is in) go to the
-// lane's private dummy word instead.
-struct LdsWordWriter {
-  uint64_t* p;      // the lane's W words
-  uint64_t* dummy;  // a private LDS word past the wave's segment
-  uint32_t words, pos;  // pos: bits produced so far
-  uint64_t acc;         // bits [64*(pos/64), pos)
-  __device__ __forceinline__ bool full() const { return pos >= 64 * words; }
-  __device__ __forceinline__ void put(uint64_t v, unsigned n) {
-    const uint32_t cnt = pos & 63, w = pos >> 6;
-    acc |= v << cnt;
-    uint64_t* dst = w < words ? p + w : dummy;
-    *dst = acc;
-    acc = cnt + n >= 64 ? (v >> 1) >> (63 - cnt) : acc;  // the bits of v that did not fit
+// maxbits % 64 == 0: the lane owns LDS words [lane*(W+4), lane*(W+4) + W) of a
+// zeroed image, plus 4 slack words.  A put ORs its bits in at the running bit
+// position (ds_or_b64 on the two words it can touch), so consecutive puts do
+// not form a read-modify-write chain through an accumulator and need no
+// flush branch; the coder's only serial state is `pos`.  Once W words are
+// filled the block is full; what the coder still produces (it finishes the
+// plane it is in, at most 128 bits + one straddled word) lands in the slack,
+// which the copy-out skips.
+constexpr uint32_t kSlackWords = 4;
+struct LdsOrWriter {
+  uint64_t* p;          // the lane's W + kSlackWords words, zeroed
+  uint32_t pos, lim;    // bits produced; 64 * W
+  __device__ __forceinline__ bool full() const { return pos >= lim; }
+  __device__ __forceinline__ void put(uint64_t v, unsigned n) {  // v < 2^n
+    const uint32_t w = pos >> 6, sh = pos & 63;
+    atomicOr((unsigned long long*)&p[w], (unsigned long long)(v << sh));
+    atomicOr((unsigned long long*)&p[w + 1], (unsigned long long)((v >> 1) >> (63 - sh)));
     pos += n;
   }
-  __device__ __forceinline__ void zero_bit() { put(0, 1); }
-  __device__ __forceinline__ void finish() {
-    for (uint32_t w = pos >> 6; w < words; w++) {
-      p[w] = acc;
-      acc = 0;
-    }
-  }
+  __device__ __forceinline__ void zero_bit() { pos++; }
+  __device__ __forceinline__ void finish() {}
 };
 
 // general maxbits: the lane's bits are [pos0, end) of the wave's segment;
@@ -119,50 +121,31 @@ struct LdsBitWriter {
   }
 };
 
-// Window over the wave's LDS stream image: w0..w5 = words base .. base+5, the
-// reading position at bit s of w0; peek()/peek2() use w0..w2.  skip() (up to
-// 128 bits, i.e. a whole plane at once) is branch-free: it shifts the window
-// by 0, 1 or 2 words and re-reads words base+4 and base+5 -- reads whose values
-// are first needed at the NEXT skip, so they never stall the lane.
+// Reader over the wave's LDS stream image.  The position is a plain bit
+// offset (skip() is one add); peek2() reads the five dwords covering bits
+// [pos, pos + 128) and funnels them into place with v_alignbit_b32, once per
+// plane.  Its only cost is the LDS latency between one plane's end and the
+// next one's start, which the other waves on the SIMD fill.
 struct LdsReader {
-  const uint64_t* lds;
-  uint64_t w0, w1, w2, w3, w4, w5;
-  uint32_t s, base;
-  __device__ __forceinline__ void init(uint32_t bitpos) {
-    base = bitpos >> 6;
-    s = bitpos & 63;
-    w0 = lds[base];
-    w1 = lds[base + 1];
-    w2 = lds[base + 2];
-    w3 = lds[base + 3];
-    w4 = lds[base + 4];
-    w5 = lds[base + 5];
-  }
-  __device__ __forceinline__ uint64_t peek() const { return (w0 >> s) | ((w1 << 1) << (63 - s)); }
+  const uint32_t* lds32;
+  uint32_t pos;
+  __device__ __forceinline__ void init(uint32_t bitpos) { pos = bitpos; }
   __device__ __forceinline__ void peek2(uint64_t& a, uint64_t& b) const {
-    a = (w0 >> s) | ((w1 << 1) << (63 - s));
-    b = (w1 >> s) | ((w2 << 1) << (63 - s));
+    const uint32_t d = pos >> 5, sh = pos & 31;
+    const uint32_t x0 = lds32[d], x1 = lds32[d + 1], x2 = lds32[d + 2], x3 = lds32[d + 3],
+                   x4 = lds32[d + 4];
+    a = (uint64_t)__builtin_amdgcn_alignbit(x1, x0, sh) |
+        ((uint64_t)__builtin_amdgcn_alignbit(x2, x1, sh) << 32);
+    b = (uint64_t)__builtin_amdgcn_alignbit(x3, x2, sh) |
+        ((uint64_t)__builtin_amdgcn_alignbit(x4, x3, sh) << 32);
   }
-  __device__ __forceinline__ void skip(unsigned n) {  // n <= 128
-    s += n;
-    const uint32_t adv = s >> 6;
-    s &= 63;
-    // two one-word steps (a nested select would be turned into a
-    // runtime-indexed window in scratch memory)
-    const bool a1 = adv != 0, a2 = adv > 1;
-    w0 = a1 ? w1 : w0;
-    w1 = a1 ? w2 : w1;
-    w2 = a1 ? w3 : w2;
-    w3 = a1 ? w4 : w3;
-    w4 = a1 ? w5 : w4;
-    w0 = a2 ? w1 : w0;
-    w1 = a2 ? w2 : w1;
-    w2 = a2 ? w3 : w2;
-    w3 = a2 ? w4 : w3;
-    base += adv;
-    w4 = lds[base + 4];
-    w5 = lds[base + 5];
+  __device__ __forceinline__ uint64_t peek() const {
+    const uint32_t d = pos >> 5, sh = pos & 31;
+    const uint32_t x0 = lds32[d], x1 = lds32[d + 1], x2 = lds32[d + 2];
+    return (uint64_t)__builtin_amdgcn_alignbit(x1, x0, sh) |
+           ((uint64_t)__builtin_amdgcn_alignbit(x2, x1, sh) << 32);
   }
+  __device__ __forceinline__ void skip(unsigned n) { pos += n; }
 };
 
 // ---------------------------------------------------------------------------
@@ -288,17 +271,20 @@ __global__ __launch_bounds__(kLanes, 4) void zfp_encode(const Scalar* __restrict
   const uint32_t lane = threadIdx.x;
   const uint32_t b = wave * kLanes + lane;
   ZFP_STAMP_HWID();
+  ZFP_STAMP_REAL(8);
   ZFP_STAMP(0);
   if constexpr (!ALIGNED) {
     for (uint32_t j = lane; j < g.maxbits + 2; j += kLanes) lds[j] = 0;
     __syncthreads();
   }
+  const uint32_t W = g.maxbits >> 6, WS = W + kSlackWords;  // ALIGNED: lane stride in words
   if (b < g.nblocks) {
     Scalar f[N];
     gather<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
     if constexpr (ALIGNED) {
-      const uint32_t W = g.maxbits >> 6;
-      LdsWordWriter wr{lds + lane * W, lds + (size_t)kLanes * W + lane, W, 0, 0};
+      uint64_t* mine = lds + (size_t)lane * WS;
+      for (uint32_t j = 0; j < WS; j++) mine[j] = 0;  // own words only: no barrier
+      LdsOrWriter wr{mine, 0, 64 * W};
       encode_block<Scalar, DIMS>(f, g.maxbits, wr);
     } else {
       LdsBitWriter wr{lds, lane * g.maxbits, (lane + 1) * g.maxbits, 0, 0};
@@ -309,7 +295,22 @@ __global__ __launch_bounds__(kLanes, 4) void zfp_encode(const Scalar* __restrict
   const uint32_t nb = min((uint32_t)kLanes, g.nblocks - wave * kLanes);
   const uint32_t nwords = (nb * g.maxbits + 63) >> 6;
   uint64_t* out = stream + (size_t)wave * g.maxbits;
-  if (g.vec_io) {  // 16-byte aligned segment
+  if constexpr (ALIGNED) {
+    // stream word o = word j of lane l's block, l = o / W (exact in float for
+    // o < 8000, W <= 125: (o + 1/2) / W stays >= 0.5/W away from integers)
+    const float rw = 1.0f / (float)W;
+    if (g.vec_io && !(W & 1)) {  // 16-byte pairs, never split across lanes
+      for (uint32_t o = 2 * lane; o < nwords; o += 2 * kLanes) {
+        const uint32_t l = (uint32_t)(((float)o + 0.5f) * rw), j = o - l * W;
+        *(uint4*)&out[o] = *(const uint4*)&lds[l * WS + j];
+      }
+    } else {
+      for (uint32_t o = lane; o < nwords; o += kLanes) {
+        const uint32_t l = (uint32_t)(((float)o + 0.5f) * rw), j = o - l * W;
+        out[o] = lds[l * WS + j];
+      }
+    }
+  } else if (g.vec_io) {  // 16-byte aligned segment
     const uint32_t npairs = nwords >> 1;
     for (uint32_t j = lane; j < npairs; j += kLanes)
       ((uint4*)out)[j] = ((const uint4*)lds)[j];
@@ -318,6 +319,7 @@ __global__ __launch_bounds__(kLanes, 4) void zfp_encode(const Scalar* __restrict
     for (uint32_t j = lane; j < nwords; j += kLanes) out[j] = lds[j];
   }
   ZFP_STAMP(6);
+  ZFP_STAMP_REAL(9);
 }
 
 template <typename Scalar, int DIMS, bool FAST>
@@ -339,19 +341,21 @@ __global__ __launch_bounds__(kLanes, 4) void zfp_decode(const uint64_t* __restri
     for (uint32_t j = lane; j < nwords; j += kLanes) lds[j] = in[j];
   }
   ZFP_STAMP_HWID();
+  ZFP_STAMP_REAL(8);
   ZFP_STAMP(0);
   if (lane < 6) lds[nwords + lane] = 0;  // reader look-ahead slack
   __syncthreads();
   ZFP_STAMP(5);
   if (b < g.nblocks) {
     LdsReader rd;
-    rd.lds = lds;
+    rd.lds32 = (const uint32_t*)lds;
     rd.init(lane * g.maxbits);
     Scalar f[N];
     decode_block<Scalar, DIMS>(f, g.maxbits, rd);
     scatter<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
   }
   ZFP_STAMP(6);
+  ZFP_STAMP_REAL(9);
 }
 
 // ---------------------------------------------------------------------------
@@ -363,8 +367,10 @@ int launch_encode_t(const void* data, const Geometry& g, bool fast, uint64_t* st
   Geometry gg = g;
   gg.wave0 = wave0;
   gg.vec_io = (g.maxbits % 2 == 0) && ((uintptr_t)stream % 16 == 0);
-  const size_t lds = ((size_t)g.maxbits + kLanes) * 8;  // + the writers' dummy words
-  const bool aligned = (g.maxbits & 63) == 0;
+  const size_t lds = ((size_t)g.maxbits + kLanes * kSlackWords) * 8;  // + per-lane slack
+  // the word-aligned writer pads each lane with slack words; very large maxbits
+  // (whose padded image would pass 64 KiB of LDS) take the general writer
+  const bool aligned = (g.maxbits & 63) == 0 && lds <= 65536;
   const Scalar* d = (const Scalar*)data;
   if (fast && aligned)
     hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, true, true>), dim3(nwaves), dim3(kLanes), lds, st, d, gg, stream);

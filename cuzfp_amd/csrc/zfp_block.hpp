@@ -482,12 +482,16 @@ ZFP_HD void encode_planes(const planes<UInt, DIMS>& P, unsigned maxprec, Writer&
 // one of F by j).  Runs starting at even positions are found with one carrying
 // add (c + their start bits clears exactly those runs).
 //
-// The fast path applies when that whole code lies in the 64-bit window, inside
-// the budget, and ends below position N-1 (no implied one); otherwise -- a
-// dense plane, the block's last bits, or a one implied at N-1 -- the exact
-// sequential group loop below runs, whose trips follow the reference's
-// control flow bit for bit (including the one it deposits when the budget ends
-// inside a run, decode.c:311).
+// When the budget ends inside the code, the reference has read a prefix of
+// it: every one in the prefix is deposited, and unless the prefix ends with a
+// one, one more one is deposited at the next position (decode.c:305-311: the
+// group loop's increment runs after the budget stops the run loop) -- so the
+// prefix needs no sequential loop either.
+//
+// The fast path applies when the code (or the budget-truncated prefix of it)
+// lies in the 64-bit window and stays below position N-1; otherwise -- a
+// dense plane, or a one implied at N-1 -- the exact sequential group loop
+// below runs, whose trips follow the reference's control flow bit for bit.
 template <int DIMS, typename PW, typename Reader>
 ZFP_HD PW decode_plane(unsigned& bits, unsigned& n, Reader& rd) {
   constexpr unsigned N = 1u << (2 * DIMS);
@@ -511,14 +515,19 @@ ZFP_HD PW decode_plane(unsigned& bits, unsigned& n, Reader& rd) {
   const uint64_t F = (erun & EVEN) | (c & ~erun & ~EVEN);
   const uint64_t oddend = F & ~(c >> 1);         // a pair's one with a 0 partner
   const unsigned qe = ctz64_or_64(oddend);       // the last one of the code
-  const uint64_t Fm = F & lowmask(qe + 1);
-  const unsigned ones = (unsigned)__builtin_popcountll(Fm);
-  const unsigned plast = qe + 1 - ones;          // its plane offset from n
-  // code = "1" + c[0 .. qe+1]: qe + 3 bits, the closing 0 at c bit qe + 1 <= 62
-  const bool fast = qe <= 61 && qe + 3 <= bits && n + plast <= N - 2;
+  // complete code: "1" + c[0 .. qe+1] (qe + 3 bits, the closing 0 <= c bit 62);
+  // else the budget's prefix "1" + c[0 .. bits-2]
+  const bool complete = qe <= 61 && qe + 3 <= bits;
+  const unsigned cb = complete ? qe + 2 : bits - 1;   // c bits consumed
+  const uint64_t cm = lowmask(cb);
+  const uint64_t Fb = F & cm;                         // ones read
+  const unsigned nong = cb - (unsigned)__builtin_popcountll((Fb << 1) & cm);  // positions advanced
+  const bool lastone = cb && ((Fb >> ((cb - 1) & 63)) & 1);
+  const bool quirk = !complete && !lastone;           // the deposit after the budget ran out
+  const bool fast = complete ? n + nong <= N - 1 : (bits <= 63 && n + nong <= N - 2);
   if (__builtin_expect(!g0 || fast, 1)) {
-    uint64_t f = g0 ? Fm : 0ull;
-    PW y = 0;
+    uint64_t f = g0 ? Fb : 0ull;
+    PW y = (g0 && quirk) ? (PW)1 << (nong & (8 * sizeof(PW) - 1)) : (PW)0;
     unsigned j = 0;
     while (f) {
       const uint64_t low = f & (0 - f);
@@ -527,8 +536,8 @@ ZFP_HD PW decode_plane(unsigned& bits, unsigned& n, Reader& rd) {
       j++;
     }
     x |= y << (n & (8 * sizeof(PW) - 1));
-    const unsigned used = g0 ? qe + 3 : (grp ? 1u : 0u);
-    n += g0 ? plast + 1 : 0u;
+    const unsigned used = g0 ? cb + 1 : (grp ? 1u : 0u);
+    n += g0 ? nong + (quirk ? 1u : 0u) : 0u;
     rd.skip(m + used);
     bits -= used;
     return x;

@@ -93,9 +93,9 @@ for name, fn in (("encode", lambda: cz.encode(x, mb, out=w)), ("decode", lambda:
     torch.cuda.synchronize()
     lib.cuzfp_hip_probe_clear()
     fn(); torch.cuda.synchronize()
-    buf = np.zeros(65536 * 8, np.uint64)
+    buf = np.zeros(65536 * 10, np.uint64)
     lib.cuzfp_hip_probe_stamps(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes))
-    np.save(os.path.join(@OUTDIR@, "stamps_" + name + "_" + @FIELD@ + "_" + str(@SIZE@) + ".npy"), buf.reshape(-1, 8)[:nw])
+    np.save(os.path.join(@OUTDIR@, "stamps_" + name + "_" + @FIELD@ + "_" + str(@SIZE@) + ".npy"), buf.reshape(-1, 10)[:nw])
 print("ok")
 """
 
@@ -115,18 +115,20 @@ def stamps(size, field, outdir):
 def analyse(path, name):
     import numpy as np
     a = np.load(path).astype(np.int64)
-    hw, t = a[:, 0], a[:, 1:]
-    t0 = t[:, 0].min()
-    rel = t - t0
-    end = rel[:, 6] if name == "encode" else rel[:, 6]
-    print(f"== {name}: {len(a)} waves, span {end.max()} cycles")
+    hw, t, rt = a[:, 0], a[:, 1:8], a[:, 8:10]
+    rel = t - t[:, :1]  # s_memtime bases differ between CUs: per-wave deltas only
+    r0 = rt[:, 0].min()
+    rs, re = (rt[:, 0] - r0) * 10, (rt[:, 1] - r0) * 10  # ns (100 MHz)
+    print(f"== {name}: {len(a)} waves, span {re.max()} ns;  wave start ns p10/50/90/max "
+          f"{int(np.percentile(rs, 10))} {int(np.median(rs))} {int(np.percentile(rs, 90))} {rs.max()};"
+          f"  end ns p10/50/90/max {int(np.percentile(re, 10))} {int(np.median(re))} {int(np.percentile(re, 90))} {re.max()}")
     labels = (["start", "emax(load)", "transform", "transpose", "planes", "-", "end"] if name == "encode"
               else ["start", "planes", "transpose", "inv-xform", "-", "copy-in", "end"])
     order = [0, 1, 2, 3, 4, 6] if name == "encode" else [0, 5, 1, 2, 3, 6]
     prev = None
     for k in order:
         col = rel[:, k]
-        line = f"  {labels[k]:11s} at: min {col.min():7d} p50 {int(np.median(col)):7d} max {col.max():7d}"
+        line = f"  {labels[k]:11s}"
         if prev is not None:
             d = rel[:, k] - rel[:, prev]
             line += f"   phase: mean {int(d.mean()):6d} p50 {int(np.median(d)):6d} max {d.max():6d}"
