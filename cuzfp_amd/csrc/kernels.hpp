@@ -26,22 +26,23 @@
 // s_memtime at the codec's phase boundaries, plus its HW_ID / XCC_ID.
 #define CUZFP_STAMP_WAVES 65536
 __device__ uint64_t g_stamps[CUZFP_STAMP_WAVES * 10];
+__device__ __forceinline__ uint32_t stamp_wave() { return blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); }
 #define ZFP_STAMP(i)                                                              \
   do {                                                                            \
-    if (threadIdx.x == 0 && blockIdx.x < CUZFP_STAMP_WAVES)                      \
-      g_stamps[blockIdx.x * 10 + 1 + (i)] = __builtin_amdgcn_s_memtime();        \
+    if ((threadIdx.x & 63) == 0 && stamp_wave() < CUZFP_STAMP_WAVES)              \
+      g_stamps[stamp_wave() * 10 + 1 + (i)] = __builtin_amdgcn_s_memtime();      \
   } while (0)
 __device__ __forceinline__ void stamp_hwid() {
   uint32_t hw, xcc;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-  if (threadIdx.x == 0 && blockIdx.x < CUZFP_STAMP_WAVES)
-    g_stamps[blockIdx.x * 10] = (uint64_t)hw | ((uint64_t)xcc << 32);
+  if ((threadIdx.x & 63) == 0 && stamp_wave() < CUZFP_STAMP_WAVES)
+    g_stamps[stamp_wave() * 10] = (uint64_t)hw | ((uint64_t)xcc << 32);
 }
 // global 100 MHz clock, comparable across CUs: slot 8 = start, 9 = end
 __device__ __forceinline__ void stamp_real(int slot) {
-  if (threadIdx.x == 0 && blockIdx.x < CUZFP_STAMP_WAVES)
-    g_stamps[blockIdx.x * 10 + slot] = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63) == 0 && stamp_wave() < CUZFP_STAMP_WAVES)
+    g_stamps[stamp_wave() * 10 + slot] = __builtin_amdgcn_s_memrealtime();
 }
 #define ZFP_STAMP_REAL(slot) stamp_real(slot)
 #define ZFP_STAMP_HWID() stamp_hwid()
@@ -262,20 +263,35 @@ __device__ __forceinline__ void scatter(Scalar* __restrict__ data, const Geometr
 // ---------------------------------------------------------------------------
 // Kernels
 
+// Up to kWavesPerGroup independent waves share a workgroup (fewer workgroups
+// for the dispatcher to launch); each has its own LDS image and they never
+// synchronise with each other.  Within a wave, LDS traffic between lanes only
+// needs the wave's own LDS operations to have completed.
+constexpr int kWavesPerGroup = 4;
+
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
 template <typename Scalar, int DIMS, bool FAST, bool ALIGNED>
-__global__ __launch_bounds__(kLanes, 4) void zfp_encode(const Scalar* __restrict__ data, Geometry g,
-                                                     uint64_t* __restrict__ stream) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+__global__ __launch_bounds__(kLanes * kWavesPerGroup, 4) void zfp_encode(const Scalar* __restrict__ data,
+                                                                      Geometry g,
+                                                                      uint64_t* __restrict__ stream) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t lds_all[];
   constexpr int N = 1 << (2 * DIMS);
-  const uint32_t wave = g.wave0 + blockIdx.x;
-  const uint32_t lane = threadIdx.x;
+  const uint32_t wig = threadIdx.x >> 6;  // wave in workgroup
+  const uint32_t wave = g.wave0 + blockIdx.x * (blockDim.x >> 6) + wig;
+  if (wave >= g.wave_end) return;
+  const uint32_t lane = threadIdx.x & 63;
   const uint32_t b = wave * kLanes + lane;
+  uint64_t* lds = lds_all + (size_t)wig * g.lds_words;
   ZFP_STAMP_HWID();
   ZFP_STAMP_REAL(8);
   ZFP_STAMP(0);
   if constexpr (!ALIGNED) {
     for (uint32_t j = lane; j < g.maxbits + 2; j += kLanes) lds[j] = 0;
-    __syncthreads();
+    wave_lds_sync();
   }
   const uint32_t W = g.maxbits >> 6, WS = W + kSlackWords;  // ALIGNED: lane stride in words
   if (b < g.nblocks) {
@@ -291,7 +307,7 @@ __global__ __launch_bounds__(kLanes, 4) void zfp_encode(const Scalar* __restrict
       encode_block<Scalar, DIMS>(f, g.maxbits, wr);
     }
   }
-  __syncthreads();
+  wave_lds_sync();
   const uint32_t nb = min((uint32_t)kLanes, g.nblocks - wave * kLanes);
   const uint32_t nwords = (nb * g.maxbits + 63) >> 6;
   uint64_t* out = stream + (size_t)wave * g.maxbits;
@@ -323,13 +339,17 @@ __global__ __launch_bounds__(kLanes, 4) void zfp_encode(const Scalar* __restrict
 }
 
 template <typename Scalar, int DIMS, bool FAST>
-__global__ __launch_bounds__(kLanes, 4) void zfp_decode(const uint64_t* __restrict__ stream,
-                                                     Geometry g, Scalar* __restrict__ data) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+__global__ __launch_bounds__(kLanes * kWavesPerGroup, 4) void zfp_decode(const uint64_t* __restrict__ stream,
+                                                                      Geometry g,
+                                                                      Scalar* __restrict__ data) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t lds_all[];
   constexpr int N = 1 << (2 * DIMS);
-  const uint32_t wave = g.wave0 + blockIdx.x;
-  const uint32_t lane = threadIdx.x;
+  const uint32_t wig = threadIdx.x >> 6;
+  const uint32_t wave = g.wave0 + blockIdx.x * (blockDim.x >> 6) + wig;
+  if (wave >= g.wave_end) return;
+  const uint32_t lane = threadIdx.x & 63;
   const uint32_t b = wave * kLanes + lane;
+  uint64_t* lds = lds_all + (size_t)wig * g.lds_words;
   const uint32_t nb = min((uint32_t)kLanes, g.nblocks - wave * kLanes);
   const uint32_t nwords = (nb * g.maxbits + 63) >> 6;
   const uint64_t* in = stream + (size_t)wave * g.maxbits;
@@ -344,7 +364,7 @@ __global__ __launch_bounds__(kLanes, 4) void zfp_decode(const uint64_t* __restri
   ZFP_STAMP_REAL(8);
   ZFP_STAMP(0);
   if (lane < 6) lds[nwords + lane] = 0;  // reader look-ahead slack
-  __syncthreads();
+  wave_lds_sync();
   ZFP_STAMP(5);
   if (b < g.nblocks) {
     LdsReader rd;
@@ -361,25 +381,36 @@ __global__ __launch_bounds__(kLanes, 4) void zfp_decode(const uint64_t* __restri
 // ---------------------------------------------------------------------------
 // Launchers
 
+// waves per workgroup: as many as fit a workgroup's 64 KiB of LDS (up to 4)
+static inline uint32_t waves_per_group(uint32_t lds_words) {
+  uint32_t w = kWavesPerGroup;
+  while (w > 1 && (size_t)w * lds_words * 8 > 65536) w >>= 1;
+  return w;
+}
+
 template <typename Scalar, int DIMS>
 int launch_encode_t(const void* data, const Geometry& g, bool fast, uint64_t* stream,
                            uint32_t wave0, uint32_t nwaves, hipStream_t st) {
   Geometry gg = g;
   gg.wave0 = wave0;
+  gg.wave_end = wave0 + nwaves;
   gg.vec_io = (g.maxbits % 2 == 0) && ((uintptr_t)stream % 16 == 0);
-  const size_t lds = ((size_t)g.maxbits + kLanes * kSlackWords) * 8;  // + per-lane slack
+  gg.lds_words = g.maxbits + kLanes * kSlackWords;  // + per-lane slack
   // the word-aligned writer pads each lane with slack words; very large maxbits
   // (whose padded image would pass 64 KiB of LDS) take the general writer
-  const bool aligned = (g.maxbits & 63) == 0 && lds <= 65536;
+  const bool aligned = (g.maxbits & 63) == 0 && gg.lds_words * 8 <= 65536;
+  const uint32_t wpg = waves_per_group(gg.lds_words);
+  const dim3 grid((nwaves + wpg - 1) / wpg), block(kLanes * wpg);
+  const size_t lds = (size_t)wpg * gg.lds_words * 8;
   const Scalar* d = (const Scalar*)data;
   if (fast && aligned)
-    hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, true, true>), dim3(nwaves), dim3(kLanes), lds, st, d, gg, stream);
+    hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, true, true>), grid, block, lds, st, d, gg, stream);
   else if (fast)
-    hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, true, false>), dim3(nwaves), dim3(kLanes), lds, st, d, gg, stream);
+    hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, true, false>), grid, block, lds, st, d, gg, stream);
   else if (aligned)
-    hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, false, true>), dim3(nwaves), dim3(kLanes), lds, st, d, gg, stream);
+    hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, false, true>), grid, block, lds, st, d, gg, stream);
   else
-    hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, false, false>), dim3(nwaves), dim3(kLanes), lds, st, d, gg, stream);
+    hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, false, false>), grid, block, lds, st, d, gg, stream);
   const hipError_t e = hipGetLastError();
   t_last_hip = e;
   return e == hipSuccess ? CUZFP_SUCCESS : CUZFP_ERROR_HIP;
@@ -390,13 +421,18 @@ int launch_decode_t(const uint64_t* stream, const Geometry& g, bool fast, void* 
                            uint32_t wave0, uint32_t nwaves, hipStream_t st) {
   Geometry gg = g;
   gg.wave0 = wave0;
+  gg.wave_end = wave0 + nwaves;
   gg.vec_io = (g.maxbits % 2 == 0) && ((uintptr_t)stream % 16 == 0);
-  const size_t lds = ((size_t)g.maxbits + 6) * 8;
+  gg.lds_words = g.maxbits + 6;  // + the reader's look-ahead slack
+  gg.lds_words += gg.lds_words & 1;  // keep every wave's image 16-byte aligned
+  const uint32_t wpg = waves_per_group(gg.lds_words);
+  const dim3 grid((nwaves + wpg - 1) / wpg), block(kLanes * wpg);
+  const size_t lds = (size_t)wpg * gg.lds_words * 8;
   Scalar* d = (Scalar*)data;
   if (fast)
-    hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, true>), dim3(nwaves), dim3(kLanes), lds, st, stream, gg, d);
+    hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, true>), grid, block, lds, st, stream, gg, d);
   else
-    hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, false>), dim3(nwaves), dim3(kLanes), lds, st, stream, gg, d);
+    hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, false>), grid, block, lds, st, stream, gg, d);
   const hipError_t e = hipGetLastError();
   t_last_hip = e;
   return e == hipSuccess ? CUZFP_SUCCESS : CUZFP_ERROR_HIP;

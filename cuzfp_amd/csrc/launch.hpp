@@ -8,15 +8,17 @@
 
 namespace cuzfp {
 
-constexpr int kLanes = 64;  // blocks per workgroup = one wave64
+constexpr int kLanes = 64;  // blocks per wave64 (one per lane)
 
 struct Geometry {
   uint32_t nx, ny, nz;   // array extent (1 for unused dimensions)
   uint32_t bx, by;       // blocks along x and y
   uint32_t nblocks;      // total blocks
   uint32_t maxbits;      // bits per block
-  uint32_t wave0;        // first wave (workgroup) of this launch
+  uint32_t wave0;        // first wave of this launch
+  uint32_t wave_end;     // one past its last wave
   uint32_t vec_io;       // stream base 16-byte aligned and maxbits even
+  uint32_t lds_words;    // LDS words per wave
   int64_t sx, sy, sz;    // element strides
 };
 
