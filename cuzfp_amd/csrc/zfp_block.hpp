@@ -168,13 +168,17 @@ ZFP_HD void fwd_lift(UInt& x, UInt& y, UInt& z, UInt& w) {
   w += asr1(y); y -= asr1(w);
 }
 
+// decode.c:243-270.  Each "a += b; b <<= 1; b -= a" step is written in its
+// two-operation form b' = b - a, a' = a + b (2b - (a + b) = b - a in modular
+// arithmetic), which the compiler does not find by itself.
 template <typename UInt>
 ZFP_HD void inv_lift(UInt& x, UInt& y, UInt& z, UInt& w) {
+  UInt t;
   y += asr1(w); w -= asr1(y);
-  y += w; w <<= 1; w -= y;
-  z += x; x <<= 1; x -= z;
-  y += z; z <<= 1; z -= y;
-  w += x; x <<= 1; x -= w;
+  t = w - y; y += w; w = t;
+  t = x - z; z += x; x = t;
+  t = z - y; y += z; z = t;
+  t = x - w; w += x; x = t;
 }
 
 template <int DIMS, typename UInt>
@@ -232,17 +236,50 @@ ZFP_HD void inv_xform(UInt* p) {
 // column R*s + j of the input, i.e. plane (R*s + j) of R coefficients.  The
 // operation is an involution, so the decoder uses it unchanged.
 
+// (a & m) | (b & ~m)
+ZFP_HD uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(m), "v"(a), "v"(b));
+  return r;
+#else
+  return (a & m) | (b & ~m);
+#endif
+}
+
+// bytes of {a = bytes 0-3, b = bytes 4-7} picked by sel (v_perm_b32)
+ZFP_HD uint32_t perm_bytes(uint32_t b, uint32_t a, uint32_t sel) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_perm(b, a, sel);
+#else
+  const uint64_t v = (uint64_t)a | ((uint64_t)b << 32);
+  uint32_t r = 0;
+  for (int i = 0; i < 4; i++) r |= (uint32_t)((v >> (8 * ((sel >> (8 * i)) & 7))) & 0xff) << (8 * i);
+  return r;
+#endif
+}
+
 template <int J>
 ZFP_HD void transpose_stage(uint32_t* a, int rows) {
-  // swap the J x J off-diagonal sub-blocks of every 2J x 2J tile
+  // swap the J x J off-diagonal sub-blocks of every 2J x 2J tile:
+  //   lo' = (lo & m) | ((hi << J) & ~m),  hi' = ((lo >> J) & m) | (hi & ~m)
+  // one v_perm_b32 per word for the byte-granular stages, two ops otherwise
   constexpr uint32_t m = J == 16 ? 0x0000ffffu : J == 8 ? 0x00ff00ffu : J == 4 ? 0x0f0f0f0fu
                        : J == 2 ? 0x33333333u : 0x55555555u;
 #pragma unroll
   for (int i = 0; i < 32; i++) {
     if (i >= rows || (i & J)) continue;
     const uint32_t lo = a[i], hi = a[i + J];
-    a[i] = (lo & m) | ((hi << J) & ~m);      // v_bfi_b32
-    a[i + J] = ((lo >> J) & m) | (hi & ~m);  // v_bfi_b32
+    if constexpr (J == 16) {
+      a[i] = perm_bytes(hi, lo, 0x05040100u);
+      a[i + J] = perm_bytes(hi, lo, 0x07060302u);
+    } else if constexpr (J == 8) {
+      a[i] = perm_bytes(hi, lo, 0x06020400u);
+      a[i + J] = perm_bytes(hi, lo, 0x07030501u);
+    } else {
+      a[i] = bfi(m, lo, hi << J);
+      a[i + J] = bfi(m, lo >> J, hi);
+    }
   }
 }
 
