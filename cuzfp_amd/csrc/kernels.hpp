@@ -122,31 +122,44 @@ struct LdsBitWriter {
   }
 };
 
-// Reader over the wave's LDS stream image.  The position is a plain bit
-// offset (skip() is one add); peek2() reads the five dwords covering bits
-// [pos, pos + 128) and funnels them into place with v_alignbit_b32, once per
-// plane.  Its only cost is the LDS latency between one plane's end and the
-// next one's start, which the other waves on the SIMD fill.
+// Reader over the wave's LDS stream image.  It keeps the five dwords that
+// cover bits [pos, pos + 128) in registers: peek()/peek2() funnel them into
+// place with v_alignbit_b32, and skip() moves the bit offset and issues the
+// LDS reads for the new position at once.  The plane decoder skips as soon as
+// it knows where the next plane starts -- before it places the plane's ones --
+// so those reads land while it still has work to do.
 struct LdsReader {
   const uint32_t* lds32;
   uint32_t pos;
-  __device__ __forceinline__ void init(uint32_t bitpos) { pos = bitpos; }
+  uint32_t x0, x1, x2, x3, x4;
+  __device__ __forceinline__ void load() {
+    const uint32_t d = pos >> 5;
+    x0 = lds32[d];
+    x1 = lds32[d + 1];
+    x2 = lds32[d + 2];
+    x3 = lds32[d + 3];
+    x4 = lds32[d + 4];
+  }
+  __device__ __forceinline__ void init(uint32_t bitpos) {
+    pos = bitpos;
+    load();
+  }
   __device__ __forceinline__ void peek2(uint64_t& a, uint64_t& b) const {
-    const uint32_t d = pos >> 5, sh = pos & 31;
-    const uint32_t x0 = lds32[d], x1 = lds32[d + 1], x2 = lds32[d + 2], x3 = lds32[d + 3],
-                   x4 = lds32[d + 4];
+    const uint32_t sh = pos & 31;
     a = (uint64_t)__builtin_amdgcn_alignbit(x1, x0, sh) |
         ((uint64_t)__builtin_amdgcn_alignbit(x2, x1, sh) << 32);
     b = (uint64_t)__builtin_amdgcn_alignbit(x3, x2, sh) |
         ((uint64_t)__builtin_amdgcn_alignbit(x4, x3, sh) << 32);
   }
   __device__ __forceinline__ uint64_t peek() const {
-    const uint32_t d = pos >> 5, sh = pos & 31;
-    const uint32_t x0 = lds32[d], x1 = lds32[d + 1], x2 = lds32[d + 2];
+    const uint32_t sh = pos & 31;
     return (uint64_t)__builtin_amdgcn_alignbit(x1, x0, sh) |
            ((uint64_t)__builtin_amdgcn_alignbit(x2, x1, sh) << 32);
   }
-  __device__ __forceinline__ void skip(unsigned n) { pos += n; }
+  __device__ __forceinline__ void skip(unsigned n) {
+    pos += n;
+    load();
+  }
 };
 
 // ---------------------------------------------------------------------------

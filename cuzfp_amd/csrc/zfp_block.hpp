@@ -563,6 +563,11 @@ ZFP_HD PW decode_plane(unsigned& bits, unsigned& n, Reader& rd) {
   const bool quirk = !complete && !lastone;           // the deposit after the budget ran out
   const bool fast = complete ? n + nong <= N - 1 : (bits <= 63 && n + nong <= N - 2);
   if (__builtin_expect(!g0 || fast, 1)) {
+    // where the next plane starts is known now: move the reader first, so its
+    // reads overlap placing this plane's ones
+    const unsigned used = g0 ? cb + 1 : (grp ? 1u : 0u);
+    rd.skip(m + used);
+    bits -= used;
     uint64_t f = g0 ? Fb : 0ull;
     PW y = (g0 && quirk) ? (PW)1 << (nong & (8 * sizeof(PW) - 1)) : (PW)0;
     unsigned j = 0;
@@ -573,10 +578,7 @@ ZFP_HD PW decode_plane(unsigned& bits, unsigned& n, Reader& rd) {
       j++;
     }
     x |= y << (n & (8 * sizeof(PW) - 1));
-    const unsigned used = g0 ? cb + 1 : (grp ? 1u : 0u);
     n += g0 ? nong + (quirk ? 1u : 0u) : 0u;
-    rd.skip(m + used);
-    bits -= used;
     return x;
   }
   // exact sequential group loop, from just after the "1" group test
