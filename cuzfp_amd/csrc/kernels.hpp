@@ -287,8 +287,15 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// Waves per SIMD the register budget is sized for: 4 (<= 128 VGPRs) in
+// general; 3D double blocks (64 x 64-bit values, 64 x 64-bit planes) need up
+// to 256 VGPRs, so 2, rather than spilling to scratch.
+template <typename Scalar, int DIMS> struct occupancy {
+  static constexpr int value = (sizeof(Scalar) == 8 && DIMS == 3) ? 2 : 4;
+};
+
 template <typename Scalar, int DIMS, bool FAST, bool ALIGNED>
-__global__ __launch_bounds__(kLanes * kWavesPerGroup, 4) void zfp_encode(const Scalar* __restrict__ data,
+__global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::value)) void zfp_encode(const Scalar* __restrict__ data,
                                                                       Geometry g,
                                                                       uint64_t* __restrict__ stream) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds_all[];
@@ -352,7 +359,7 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, 4) void zfp_encode(const S
 }
 
 template <typename Scalar, int DIMS, bool FAST>
-__global__ __launch_bounds__(kLanes * kWavesPerGroup, 4) void zfp_decode(const uint64_t* __restrict__ stream,
+__global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::value)) void zfp_decode(const uint64_t* __restrict__ stream,
                                                                       Geometry g,
                                                                       Scalar* __restrict__ data) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds_all[];

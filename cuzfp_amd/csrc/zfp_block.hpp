@@ -39,6 +39,9 @@
 #ifndef ZFP_STAMP
 #define ZFP_STAMP(i)
 #endif
+#ifndef ZFP_COUNT_PLANE  // host-side path statistics (tools/path_stats.cpp)
+#define ZFP_COUNT_PLANE(g0, fast, complete)
+#endif
 
 namespace cuzfp {
 
@@ -562,6 +565,7 @@ ZFP_HD PW decode_plane(unsigned& bits, unsigned& n, Reader& rd) {
   const bool lastone = cb && ((Fb >> ((cb - 1) & 63)) & 1);
   const bool quirk = !complete && !lastone;           // the deposit after the budget ran out
   const bool fast = complete ? n + nong <= N - 1 : (bits <= 63 && n + nong <= N - 2);
+  ZFP_COUNT_PLANE(g0, fast, complete);
   if (__builtin_expect(!g0 || fast, 1)) {
     // where the next plane starts is known now: move the reader first, so its
     // reads overlap placing this plane's ones
