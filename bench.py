@@ -34,6 +34,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "GB/s input encoded+decoded (device-resident), 3D f32 fixed-rate; % HBM peak"
+METRIC_OTHER = "GB/s input encoded+decoded (device-resident), {dims}D {dt} fixed-rate; % HBM peak"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
 
 
@@ -42,7 +43,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--size", type=int, default=256, help="per-GPU cube edge (3D)")
+    p.add_argument("--size", type=int, default=256, help="per-GPU array edge (cube edge in 3D)")
+    p.add_argument("--dims", type=int, default=3, choices=[1, 2, 3],
+                   help="1D / 2D arrays of edge --size (BASELINE configs 2D 8192^2 r2, 1D 1M r8); "
+                        "the headline workload is 3D")
     p.add_argument("--rate", type=float, default=8.0)
     p.add_argument("--dtype", default="float32", choices=["float32", "float64"])
     p.add_argument("--field", default="polynomial", choices=["polynomial", "splitmix"])
@@ -54,9 +58,10 @@ def parse():
 
 
 def cpu_baseline(a: np.ndarray, maxbits: int):
-    """Reference CPU zfp 0.5.0 (zfp_compress + zfp_decompress), slab-parallel over
-    this process's cores, on the first 64 z-planes of the workload (a bounded
-    sample: 1/4 of the 256^3 array)."""
+    """Reference CPU zfp 0.5.0 (zfp_compress + zfp_decompress, oracle/_ref) on
+    this process's host cores: the whole workload array, slab-parallel over up
+    to 16 threads, median of 30 round trips (about 10-15 core-seconds); plus one
+    core on the first quarter of the array."""
     try:
         import oracle
     except Exception:  # pragma: no cover
@@ -65,19 +70,20 @@ def cpu_baseline(a: np.ndarray, maxbits: int):
     kind = "reference"
     if ref is None:
         return None
-    sample = np.ascontiguousarray(a[:64])
+    sample = np.ascontiguousarray(a)
+    quarter = np.ascontiguousarray(a[: max(4, (a.shape[0] // 16) * 4)])
     cores = max(1, min(16, len(os.sched_getaffinity(0))))
-    reps = 5
+    reps = 30
     t0 = time.perf_counter()
     rt, enc, dec, _ = ref.time_roundtrip(sample, maxbits, threads=cores, reps=reps)
-    rt1, enc1, dec1, _ = ref.time_roundtrip(sample[:16], maxbits, threads=1, reps=3)
+    rt1, enc1, dec1, _ = ref.time_roundtrip(quarter, maxbits, threads=1, reps=3)
     wall = time.perf_counter() - t0
     nbytes = sample.nbytes
     return {"value": round(nbytes / rt / 1e9, 4), "unit": "GB/s", "cores": cores, "kind": kind,
-            "sample": f"{sample.shape[0]}x{sample.shape[1]}x{sample.shape[2]} {sample.dtype} slab of the "
-                      f"workload, maxbits {maxbits}, median of {reps} round trips, z-slab threads",
+            "sample": f"the whole {'x'.join(map(str, sample.shape))} {sample.dtype} workload array, maxbits "
+                      f"{maxbits}, median of {reps} round trips, slab threads (slowest axis)",
             "encode_GBps": round(nbytes / enc / 1e9, 4), "decode_GBps": round(nbytes / dec / 1e9, 4),
-            "single_core_GBps": round(sample[:16].nbytes / rt1 / 1e9, 4),
+            "single_core_GBps": round(quarter.nbytes / rt1 / 1e9, 4),
             "wall_s": round(wall, 2)}
 
 
@@ -103,12 +109,17 @@ def main():
 
     dtype = np.dtype(args.dtype)
     n = args.size
-    shape = (n, n, n)                                  # this rank's z-slab
-    gshape = (n * world, n, n)                         # the global array
-    maxbits = cz.rate_to_maxbits(args.rate, dtype, 3)
+    dims = args.dims
+    shape = (n,) * dims                                # this rank's slab
+    gshape = (n * world,) + (n,) * (dims - 1)          # the global array
+    maxbits = cz.rate_to_maxbits(args.rate, dtype, dims)
     # each rank's slab: planes [rank*n, (rank+1)*n) of the global field
     if args.field == "polynomial":
-        a = polynomial_slab(gshape, rank * n, (rank + 1) * n, dtype)
+        if dims == 3:
+            a = polynomial_slab(gshape, rank * n, (rank + 1) * n, dtype)
+        else:
+            from cuzfp_amd.datagen import polynomial_field
+            a = polynomial_field(shape, dtype)
     else:
         a = splitmix_uniform(shape, dtype, seed=42 + rank)
     x = torch.from_numpy(a).to(dev)
@@ -146,7 +157,7 @@ def main():
     gpath = os.path.join(ROOT, "tests", "golden", "golden.json")
     key = {("float32", 8.0): "baseline/3d_f32_256_r8", ("float64", 16.0): "baseline/3d_f64_256_r16"}.get(
         (args.dtype, args.rate))
-    if key and n == 256 and world == 1 and os.path.exists(gpath):
+    if key and dims == 3 and n == 256 and world == 1 and os.path.exists(gpath):
         rec = json.load(open(gpath))["cases"].get(f"{key}/{args.field}")
         if rec:
             got = hashlib.sha256(words.cpu().numpy().tobytes()).hexdigest()
@@ -229,7 +240,7 @@ def main():
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            wk = f"3d_{args.dtype}_{n}^3_rate{args.rate:g}"
+            wk = f"{dims}d_{args.dtype}_{n}^{dims}_rate{args.rate:g}"
             if tj.get("workload") == wk:
                 traffic = tj.get(dominant + "_hbm_bytes_per_launch")
         except Exception:
@@ -257,7 +268,8 @@ def main():
                          "note": "pinned host buffers, PCIe-inclusive (cuzfp_hip_compress_host/decompress_host)"}
         cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(a, maxbits)
         result = {
-            "metric": METRIC,
+            "metric": METRIC if (dims == 3 and args.dtype == "float32") else
+                      METRIC_OTHER.format(dims=dims, dt="f32" if args.dtype == "float32" else "f64"),
             "value": round(value, 2),
             "unit": "GB/s",
             "n_gpus": world,
@@ -269,7 +281,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32" if args.dtype == "float32" else "f64",
             "data": f"synthetic ({'testzfp polynomial field' if args.field == 'polynomial' else 'splitmix64 uniform [-1,1)'})",
-            "config": {"workload": f"3d_{args.dtype}_{n}^3_rate{args.rate:g}", "shape_per_gpu": list(shape),
+            "config": {"workload": f"{dims}d_{args.dtype}_{n}^{dims}_rate{args.rate:g}", "shape_per_gpu": list(shape),
                        "global_shape": list(gshape), "maxbits": maxbits, "rate": args.rate,
                        "parallelism": f"z-slab x{world}", "stream_bytes_per_gpu": s_bytes},
             "pct_hbm_peak": round(100.0 * value / world * (enc_bytes + dec_bytes) / n_in / HBM_PEAK_GBS, 2),

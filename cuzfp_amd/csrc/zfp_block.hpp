@@ -528,52 +528,99 @@ ZFP_HD void encode_planes(const planes<UInt, DIMS>& P, unsigned maxprec, Writer&
 // group loop's increment runs after the budget stops the run loop) -- so the
 // prefix needs no sequential loop either.
 //
-// The fast path applies when the code (or the budget-truncated prefix of it)
-// lies in the 64-bit window and stays below position N-1; otherwise -- a
-// dense plane, or a one implied at N-1 -- the exact sequential group loop
-// below runs, whose trips follow the reference's control flow bit for bit.
+// Codes longer than one 64-bit window (dense planes) are taken in chunks,
+// each consumed up to its last whole (one, "1") pair.  The plane in which the
+// last coefficient becomes significant ends with a run of zeros up to position
+// N-1 and an implied one; that end is also found without a per-bit loop.
+// Whatever is left (a code the chunking cannot split) runs the exact
+// sequential group loop, whose trips follow the reference's control flow bit
+// for bit.  tests/test_emulation.py and test_gpu_parity.py decode arbitrary
+// bit streams against the oracle to exercise every path.
 template <int DIMS, typename PW, typename Reader>
 ZFP_HD PW decode_plane(unsigned& bits, unsigned& n, Reader& rd) {
   constexpr unsigned N = 1u << (2 * DIMS);
   constexpr uint64_t EVEN = 0x5555555555555555ull;
+  constexpr unsigned PWB = 8 * sizeof(PW);
   uint64_t v0, v1;
   rd.peek2(v0, v1);  // stream bits [pos, pos + 128)
   const unsigned m = umin(n, bits);
   PW x = (PW)(v0 & lowmask(m));
   bits -= m;
   // The group part exists while positions and budget remain; then m <= n < N
-  // <= 64 and m < 64, and `win` is the window at the leading group test.  All
-  // of it is computed for every lane and selected, so the wave does not branch
-  // on the data (a lane without group part, or with a "0" group test, gets an
-  // empty F and consumes 0 or 1 bit).
+  // <= 64 and m < 64, and `win` is the window at the leading group test.
   const bool grp = n < N && bits;
   const uint64_t win = (v0 >> (m & 63)) | ((v1 << 1) << (63 - (m & 63)));
-  const bool g0 = grp && (win & 1);
-  const uint64_t c = win >> 1;                   // 63 valid bits
-  const uint64_t starts = c & ~(c << 1);
-  const uint64_t erun = c & ~(c + (starts & EVEN));
-  const uint64_t F = (erun & EVEN) | (c & ~erun & ~EVEN);
-  const uint64_t oddend = F & ~(c >> 1);         // a pair's one with a 0 partner
-  const unsigned qe = ctz64_or_64(oddend);       // the last one of the code
-  // complete code: "1" + c[0 .. qe+1] (qe + 3 bits, the closing 0 <= c bit 62);
-  // else the budget's prefix "1" + c[0 .. bits-2]
-  const bool complete = qe <= 61 && qe + 3 <= bits;
-  const unsigned cb = complete ? qe + 2 : bits - 1;   // c bits consumed
-  const uint64_t cm = lowmask(cb);
-  const uint64_t Fb = F & cm;                         // ones read
-  const unsigned nong = cb - (unsigned)__builtin_popcountll((Fb << 1) & cm);  // positions advanced
-  const bool lastone = cb && ((Fb >> ((cb - 1) & 63)) & 1);
-  const bool quirk = !complete && !lastone;           // the deposit after the budget ran out
-  const bool fast = complete ? n + nong <= N - 1 : (bits <= 63 && n + nong <= N - 2);
-  ZFP_COUNT_PLANE(g0, fast, complete);
-  if (__builtin_expect(!g0 || fast, 1)) {
-    // where the next plane starts is known now: move the reader first, so its
-    // reads overlap placing this plane's ones
-    const unsigned used = g0 ? cb + 1 : (grp ? 1u : 0u);
-    rd.skip(m + used);
-    bits -= used;
-    uint64_t f = g0 ? Fb : 0ull;
-    PW y = (g0 && quirk) ? (PW)1 << (nong & (8 * sizeof(PW) - 1)) : (PW)0;
+  const unsigned lead = grp ? 1u : 0u;
+  bits -= lead;
+  unsigned step = m + lead;      // bits read but not yet skipped
+  uint64_t c = win >> 1;         // the code after the "1" group test
+  unsigned valid = 63;           // valid bits in c
+  bool more = grp && (win & 1);
+  bool slow = false;
+  // One trip per 64-bit chunk of code (one for all but dense planes).  A
+  // chunk that neither ends the code nor the budget is consumed up to its
+  // last whole (one, "1") pair, and the next chunk starts at a segment.
+  while (more) {
+    const uint64_t starts = c & ~(c << 1);
+    const uint64_t erun = c & ~(c + (starts & EVEN));
+    // segment ones (Fall), and those whose partner bit is inside the chunk (F)
+    const uint64_t Fall = (erun & EVEN) | (c & ~erun & ~EVEN);
+    const uint64_t F = Fall & lowmask(valid - 1);
+    const uint64_t oddend = F & ~(c >> 1);       // a one with a 0 partner
+    const unsigned qe = ctz64_or_64(oddend);     // >= 64 if none
+    const bool complete = qe < 64 && qe + 2 <= bits;    // code ends here: c[0 .. qe+1]
+    const bool limited = !complete && bits <= valid;    // budget ends here: c[0 .. bits-1]
+    const unsigned ql = F ? 63u - (unsigned)__builtin_clzll(F) : 0u;
+    const unsigned cb = complete ? qe + 2 : limited ? bits : ql + 2;  // chunk bits consumed
+    const uint64_t cm = lowmask(cb);
+    const uint64_t Fb = Fall & cm;               // ones read
+    const unsigned nong = cb - (unsigned)__builtin_popcountll((Fb << 1) & cm);  // positions advanced
+    const bool lastone = cb && ((Fb >> ((cb - 1) & 63)) & 1);
+    const bool quirk = limited && !lastone;      // the deposit after the budget ran out
+    const bool ok = complete ? n + nong <= N - 1 : (limited || F) && n + nong <= N - 2;
+    ZFP_COUNT_PLANE(true, ok, complete);
+    if (__builtin_expect(!ok, 0)) {
+      // The code reaches position N-1 before it ends: there the one is
+      // implied and nothing more is read (the plane where coefficient N-1
+      // becomes significant).  The real ones are F's bits below plane offset
+      // N'-1 (N' = N - n); the code is those pairs and the zeros up to offset
+      // N'-2: N'-1 + ones bits.
+      const int np = (int)(N - n);
+      uint64_t f = F, fr = 0;
+      PW y = 0;
+      unsigned j = 0;
+      while (f) {
+        const uint64_t low = f & (0 - f);
+        if ((int)(ctz64(low) - j) > np - 2) break;
+        y |= (PW)(low >> j);
+        fr |= low;
+        f ^= low;
+        j++;
+      }
+      const unsigned e = (unsigned)np - 1 + j;
+      // every one in c[0 .. e) must be one of those pairs (a one whose partner
+      // lies past the chunk is not in F)
+      if (e > bits || e > valid || ((c ^ fr ^ (fr << 1)) & lowmask(e))) {
+        slow = true;
+        break;
+      }
+      x |= (y | ((PW)1 << ((unsigned)(np - 1) & (PWB - 1)))) << (n & (PWB - 1));
+      n = N;
+      step += e;
+      bits -= e;
+      rd.skip(step);
+      step = 0;
+      break;
+    }
+    more = !complete && !limited;
+    step += cb;
+    bits -= cb;
+    if (!more) {  // the next plane's start is known: move the reader now, so
+      rd.skip(step);  // its reads overlap placing this chunk's ones
+      step = 0;
+    }
+    uint64_t f = Fb;
+    PW y = quirk ? (PW)1 << (nong & (PWB - 1)) : (PW)0;
     unsigned j = 0;
     while (f) {
       const uint64_t low = f & (0 - f);
@@ -581,17 +628,23 @@ ZFP_HD PW decode_plane(unsigned& bits, unsigned& n, Reader& rd) {
       f ^= low;
       j++;
     }
-    x |= y << (n & (8 * sizeof(PW) - 1));
-    n += g0 ? nong + (quirk ? 1u : 0u) : 0u;
-    return x;
+    x |= y << (n & (PWB - 1));
+    n += nong + (quirk ? 1u : 0u);
+    if (more) {
+      rd.skip(step);
+      step = 0;
+      c = rd.peek();
+      valid = 64;
+    }
   }
-  // exact sequential group loop, from just after the "1" group test
-  rd.skip(m);
-  rd.skip(1);
-  bits -= 1;
-  bool more = true;
-  // one trip per new one: the run of zeros, the one (unless implied at
-  // position N-1) and the following group test, all from one window
+  if (step) rd.skip(step);
+  if (__builtin_expect(!slow, 1)) return x;
+  // Exact sequential group loop from the start of a segment (a dense plane
+  // whose code outruns its chunks, or a one implied at position N-1): one trip
+  // per new one -- the run of zeros, the one (unless implied) and the
+  // following group test, all from one window -- following the reference's
+  // control flow bit for bit.
+  more = true;
   while (more) {
     const uint64_t w = rd.peek();
     const unsigned lim = umin(N - 1 - n, bits);   // zeros we may still read

@@ -120,3 +120,26 @@ def test_emulation_extremes(emu, restatement):
             assert np.array_equal(emu_compress(emu, a, mb), s)
             d = emu_decompress(emu, s, a.shape, a.dtype, mb)
             assert np.array_equal(d.view(np.uint8), restatement.decompress(s, a.shape, a.dtype, mb).view(np.uint8))
+
+
+@pytest.mark.parametrize("dims", [1, 2, 3])
+@pytest.mark.parametrize("dtype", [np.float32, np.float64, np.int32, np.int64])
+def test_emulation_random_streams(emu, restatement, dims, dtype):
+    """Arbitrary bit streams (not encoder output) decoded the reference's way:
+    dense and sparse bit patterns drive the decoder through every path of its
+    plane step -- chunked dense codes, the one implied at position N-1, the
+    budget ending inside a run (decode.c:311), the sequential fallback."""
+    rng = np.random.default_rng(7 + dims + 10 * np.dtype(dtype).itemsize)
+    for trial in range(24):
+        shape = tuple(int(rng.integers(1, 24 if dims < 3 else 12)) for _ in range(dims))
+        mb = int(rng.choice([12, 33, 63, 64, 65, 127, 128, 191, 256, 512, 777, 1024, 2000]))
+        if np.dtype(dtype) == np.float64 and mb < 12:
+            mb = 12
+        nb = int(np.prod([(s + 3) // 4 for s in shape]))
+        words = (nb * mb + 63) // 64
+        density = (0.5, 0.1, 0.9, 0.03, 0.97, 0.7)[trial % 6]
+        bits = rng.random(words * 64) < density
+        s = np.packbits(bits.reshape(-1, 8)[:, ::-1], axis=1).reshape(-1).view(np.uint64).copy()
+        want = restatement.decompress(s, shape, dtype, mb)
+        got = emu_decompress(emu, s, shape, dtype, mb)
+        assert np.array_equal(got.view(np.uint8), want.view(np.uint8)), (shape, mb, density)

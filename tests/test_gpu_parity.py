@@ -259,3 +259,31 @@ def test_host_pipeline(cuda, restatement, shape, dtype, rate, pinned):
         assert np.array_equal(s, ref)
         y = cz.decompress_host(s, shape, dtype, mb, nstreams=nstreams)
         assert np.array_equal(y, restatement.decompress(ref, shape, dtype, mb))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dims", [1, 2, 3])
+@pytest.mark.parametrize("dtype", [np.float32, np.float64, np.int32, np.int64])
+def test_random_streams(cuda, restatement, dims, dtype):
+    """Arbitrary bit streams decoded on the GPU exactly as the reference decodes
+    them: dense / sparse bit patterns reach every path of the plane decoder
+    (chunked dense codes, the one implied at position N-1, the budget ending
+    inside a run, the sequential fallback) in many lanes of a wave at once."""
+    import torch
+    rng = np.random.default_rng(31 + dims + 10 * np.dtype(dtype).itemsize)
+    for trial in range(12):
+        shape = tuple(int(rng.integers(1, 40 if dims < 3 else 20)) for _ in range(dims))
+        if trial == 0:
+            shape = (64,) * dims if dims < 3 else (32, 32, 32)
+        mb = int(rng.choice([12, 33, 63, 64, 65, 127, 128, 191, 256, 512, 777, 1024, 2000]))
+        nb = int(np.prod([(s + 3) // 4 for s in shape]))
+        words = (nb * mb + 63) // 64
+        density = (0.5, 0.1, 0.9, 0.03, 0.97, 0.7)[trial % 6]
+        bits = rng.random(words * 64) < density
+        s = np.packbits(bits.reshape(-1, 8)[:, ::-1], axis=1).reshape(-1).view(np.uint64).copy()
+        want = restatement.decompress(s, shape, dtype, mb)
+        d = torch.from_numpy(s.view(np.int64)).to(cuda)
+        tdt = {np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64,
+               np.dtype(np.int32): torch.int32, np.dtype(np.int64): torch.int64}[np.dtype(dtype)]
+        got = cz.decode(d, shape, tdt, mb).cpu().numpy()
+        assert np.array_equal(got.view(np.uint8), want.view(np.uint8)), (shape, mb, density)
