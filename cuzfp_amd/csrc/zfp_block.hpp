@@ -536,10 +536,58 @@ ZFP_HD void encode_planes(const planes<UInt, DIMS>& P, unsigned maxprec, Writer&
 // sequential group loop, whose trips follow the reference's control flow bit
 // for bit.  tests/test_emulation.py and test_gpu_parity.py decode arbitrary
 // bit streams against the oracle to exercise every path.
+// One chunk of a plane's group code: c holds `valid` code bits starting at a
+// segment (its first bit is a run of zeros or a one).  Returns false if the
+// chunk neither ends the code nor can be split at a pair (the caller then
+// takes the sequential loop).  Otherwise sets cb (code bits consumed), Fb (the
+// ones read, at their code positions), nong (plane positions advanced), quirk
+// (a one deposited after the budget ran out) and done (the code ended here).
+struct chunk_parse {
+  uint64_t Fb;
+  unsigned cb, nong;
+  bool quirk, done;
+};
+
+template <int N>
+ZFP_HD bool parse_chunk(uint64_t c, unsigned valid, unsigned bits, unsigned n, chunk_parse& r) {
+  constexpr uint64_t EVEN = 0x5555555555555555ull;
+  const uint64_t starts = c & ~(c << 1);
+  const uint64_t erun = c & ~(c + (starts & EVEN));
+  const uint64_t Fall = (erun & EVEN) | (c & ~erun & ~EVEN);  // segment ones
+  const uint64_t F = Fall & lowmask(valid - 1);                // ... with their partner inside
+  const uint64_t oddend = F & ~(c >> 1);                       // a one with a 0 partner
+  const unsigned qe = ctz64_or_64(oddend);                     // >= 64 if none
+  const bool complete = qe < 64 && qe + 2 <= bits;             // code ends: c[0 .. qe+1]
+  const bool limited = !complete && bits <= valid;             // budget ends: c[0 .. bits-1]
+  const unsigned ql = F ? 63u - (unsigned)__builtin_clzll(F) : 0u;
+  r.cb = complete ? qe + 2 : limited ? bits : ql + 2;
+  const uint64_t cm = lowmask(r.cb);
+  r.Fb = Fall & cm;
+  r.nong = r.cb - (unsigned)__builtin_popcountll((r.Fb << 1) & cm);
+  const bool lastone = r.cb && ((r.Fb >> ((r.cb - 1) & 63)) & 1);
+  r.quirk = limited && !lastone;
+  r.done = complete || limited;
+  return complete ? n + r.nong <= N - 1 : (limited || F) && n + r.nong <= N - 2;
+}
+
+// the j-th one of Fb moved down by j (the g bits below it removed), plus the
+// one deposited after the budget ran out
+template <typename PW>
+ZFP_HD PW place_ones(uint64_t f, bool quirk, unsigned nong) {
+  PW y = quirk ? (PW)1 << (nong & (8 * sizeof(PW) - 1)) : (PW)0;
+  unsigned j = 0;
+  while (f) {
+    const uint64_t low = f & (0 - f);
+    y |= (PW)(low >> j);
+    f ^= low;
+    j++;
+  }
+  return y;
+}
+
 template <int DIMS, typename PW, typename Reader>
 ZFP_HD PW decode_plane(unsigned& bits, unsigned& n, Reader& rd) {
   constexpr unsigned N = 1u << (2 * DIMS);
-  constexpr uint64_t EVEN = 0x5555555555555555ull;
   constexpr unsigned PWB = 8 * sizeof(PW);
   uint64_t v0, v1;
   rd.peek2(v0, v1);  // stream bits [pos, pos + 128)
@@ -547,104 +595,82 @@ ZFP_HD PW decode_plane(unsigned& bits, unsigned& n, Reader& rd) {
   PW x = (PW)(v0 & lowmask(m));
   bits -= m;
   // The group part exists while positions and budget remain; then m <= n < N
-  // <= 64 and m < 64, and `win` is the window at the leading group test.
+  // <= 64 and m < 64, and `win` is the window at the leading group test.  The
+  // first chunk is computed for every lane and selected, so the wave does not
+  // branch on the data (a lane without group part, or with a "0" group test,
+  // places nothing and consumes 0 or 1 bit).
   const bool grp = n < N && bits;
   const uint64_t win = (v0 >> (m & 63)) | ((v1 << 1) << (63 - (m & 63)));
+  const bool g0 = grp && (win & 1);
   const unsigned lead = grp ? 1u : 0u;
   bits -= lead;
-  unsigned step = m + lead;      // bits read but not yet skipped
-  uint64_t c = win >> 1;         // the code after the "1" group test
-  unsigned valid = 63;           // valid bits in c
-  bool more = grp && (win & 1);
-  bool slow = false;
-  // One trip per 64-bit chunk of code (one for all but dense planes).  A
-  // chunk that neither ends the code nor the budget is consumed up to its
-  // last whole (one, "1") pair, and the next chunk starts at a segment.
-  while (more) {
+  chunk_parse r;
+  const bool ok = parse_chunk<N>(win >> 1, 63, bits, n, r);
+  ZFP_COUNT_PLANE(g0, ok && r.done, r.cb);
+  if (__builtin_expect(!g0 || (ok && r.done), 1)) {
+    // where the next plane starts is known now: move the reader first, so its
+    // reads overlap placing this plane's ones
+    const unsigned used = g0 ? r.cb : 0u;
+    rd.skip(m + lead + used);
+    bits -= used;
+    x |= place_ones<PW>(g0 ? r.Fb : 0ull, g0 && r.quirk, r.nong) << (n & (PWB - 1));
+    n += g0 ? r.nong + (r.quirk ? 1u : 0u) : 0u;
+    return x;
+  }
+  // Rare: a dense code longer than the first chunk, or a code that reaches
+  // position N-1.  Chunks are consumed up to their last whole (one, "1") pair
+  // while that is possible.
+  rd.skip(m + lead);
+  uint64_t c = win >> 1;
+  unsigned valid = 63;
+  bool okc = ok;
+  while (okc) {
+    rd.skip(r.cb);
+    bits -= r.cb;
+    x |= place_ones<PW>(r.Fb, r.quirk, r.nong) << (n & (PWB - 1));
+    n += r.nong + (r.quirk ? 1u : 0u);
+    if (r.done) return x;
+    c = rd.peek();
+    valid = 64;
+    okc = parse_chunk<N>(c, valid, bits, n, r);
+  }
+  {
+    // The code reaches position N-1 before it ends: there the one is implied
+    // and nothing more is read (the plane in which coefficient N-1 becomes
+    // significant).  The real ones are the chunk's segment ones below plane
+    // offset N'-1 (N' = N - n); the code is those pairs plus the zeros up to
+    // offset N'-2: N'-1 + ones bits, and every one in it must belong to
+    // those pairs (a one whose partner lies past the chunk is not in F).
+    constexpr uint64_t EVEN = 0x5555555555555555ull;
     const uint64_t starts = c & ~(c << 1);
     const uint64_t erun = c & ~(c + (starts & EVEN));
-    // segment ones (Fall), and those whose partner bit is inside the chunk (F)
-    const uint64_t Fall = (erun & EVEN) | (c & ~erun & ~EVEN);
-    const uint64_t F = Fall & lowmask(valid - 1);
-    const uint64_t oddend = F & ~(c >> 1);       // a one with a 0 partner
-    const unsigned qe = ctz64_or_64(oddend);     // >= 64 if none
-    const bool complete = qe < 64 && qe + 2 <= bits;    // code ends here: c[0 .. qe+1]
-    const bool limited = !complete && bits <= valid;    // budget ends here: c[0 .. bits-1]
-    const unsigned ql = F ? 63u - (unsigned)__builtin_clzll(F) : 0u;
-    const unsigned cb = complete ? qe + 2 : limited ? bits : ql + 2;  // chunk bits consumed
-    const uint64_t cm = lowmask(cb);
-    const uint64_t Fb = Fall & cm;               // ones read
-    const unsigned nong = cb - (unsigned)__builtin_popcountll((Fb << 1) & cm);  // positions advanced
-    const bool lastone = cb && ((Fb >> ((cb - 1) & 63)) & 1);
-    const bool quirk = limited && !lastone;      // the deposit after the budget ran out
-    const bool ok = complete ? n + nong <= N - 1 : (limited || F) && n + nong <= N - 2;
-    ZFP_COUNT_PLANE(true, ok, complete);
-    if (__builtin_expect(!ok, 0)) {
-      // The code reaches position N-1 before it ends: there the one is
-      // implied and nothing more is read (the plane where coefficient N-1
-      // becomes significant).  The real ones are F's bits below plane offset
-      // N'-1 (N' = N - n); the code is those pairs and the zeros up to offset
-      // N'-2: N'-1 + ones bits.
-      const int np = (int)(N - n);
-      uint64_t f = F, fr = 0;
-      PW y = 0;
-      unsigned j = 0;
-      while (f) {
-        const uint64_t low = f & (0 - f);
-        if ((int)(ctz64(low) - j) > np - 2) break;
-        y |= (PW)(low >> j);
-        fr |= low;
-        f ^= low;
-        j++;
-      }
-      const unsigned e = (unsigned)np - 1 + j;
-      // every one in c[0 .. e) must be one of those pairs (a one whose partner
-      // lies past the chunk is not in F)
-      if (e > bits || e > valid || ((c ^ fr ^ (fr << 1)) & lowmask(e))) {
-        slow = true;
-        break;
-      }
-      x |= (y | ((PW)1 << ((unsigned)(np - 1) & (PWB - 1)))) << (n & (PWB - 1));
-      n = N;
-      step += e;
-      bits -= e;
-      rd.skip(step);
-      step = 0;
-      break;
-    }
-    more = !complete && !limited;
-    step += cb;
-    bits -= cb;
-    if (!more) {  // the next plane's start is known: move the reader now, so
-      rd.skip(step);  // its reads overlap placing this chunk's ones
-      step = 0;
-    }
-    uint64_t f = Fb;
-    PW y = quirk ? (PW)1 << (nong & (PWB - 1)) : (PW)0;
+    const uint64_t F = ((erun & EVEN) | (c & ~erun & ~EVEN)) & lowmask(valid - 1);
+    const int np = (int)(N - n);
+    uint64_t f = F, fr = 0;
+    PW y = 0;
     unsigned j = 0;
     while (f) {
       const uint64_t low = f & (0 - f);
+      if ((int)(ctz64(low) - j) > np - 2) break;
       y |= (PW)(low >> j);
+      fr |= low;
       f ^= low;
       j++;
     }
-    x |= y << (n & (PWB - 1));
-    n += nong + (quirk ? 1u : 0u);
-    if (more) {
-      rd.skip(step);
-      step = 0;
-      c = rd.peek();
-      valid = 64;
+    const unsigned e = (unsigned)np - 1 + j;
+    if (e <= bits && e <= valid && !((c ^ fr ^ (fr << 1)) & lowmask(e))) {
+      x |= (y | ((PW)1 << ((unsigned)(np - 1) & (PWB - 1)))) << (n & (PWB - 1));
+      n = N;
+      rd.skip(e);
+      bits -= e;
+      return x;
     }
   }
-  if (step) rd.skip(step);
-  if (__builtin_expect(!slow, 1)) return x;
-  // Exact sequential group loop from the start of a segment (a dense plane
-  // whose code outruns its chunks, or a one implied at position N-1): one trip
-  // per new one -- the run of zeros, the one (unless implied) and the
-  // following group test, all from one window -- following the reference's
-  // control flow bit for bit.
-  more = true;
+  // Exact sequential group loop from the start of a segment: one trip per new
+  // one -- the run of zeros, the one (unless implied) and the following group
+  // test, all from one window -- following the reference's control flow bit
+  // for bit.
+  bool more = true;
   while (more) {
     const uint64_t w = rd.peek();
     const unsigned lim = umin(N - 1 - n, bits);   // zeros we may still read

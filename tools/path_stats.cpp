@@ -8,7 +8,7 @@
 static int g_path[64];  // per-plane-call path of the current lane: 0 no group, 1 g0=0, 2 complete, 3 limited, 4 fallback
 static int g_calls;
 #define ZFP_COUNT_PLANE(g0, fast, complete) \
-  do { g_path[g_calls++ & 63] = !(g0) ? 1 : (fast) ? ((complete) ? 2 : 3) : 4; } while (0)
+  do { g_path[g_calls++ & 63] = !(g0) ? 1 : (fast) ? 2 : 4; } while (0)
 #include "../cuzfp_amd/csrc/zfp_block.hpp"
 #include <math.h>
 
