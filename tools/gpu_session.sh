@@ -55,6 +55,14 @@ for s in $STEPS; do
           python tools/kernel_probe.py ${PROBE_ARGS:-} > /dev/null 2>&1
         ok_or_stop $? counters_g$i
       done ;;
+    configs)
+      # the other BASELINE configs: 2D f32 8192^2 rate 2, 1D f32 1M rate 8 (and 1D 64M)
+      timeout -k 10 300 python bench.py --dims 2 --size 8192 --rate 2 --no-cpu-baseline --no-host-path > "$OUT/bench_2d_$TAG.json" 2>&1
+      ok_or_stop $? bench2d; tail -1 "$OUT/bench_2d_$TAG.json" | cut -c1-900
+      timeout -k 10 300 python bench.py --dims 1 --size 1048576 --rate 8 --no-cpu-baseline --no-host-path > "$OUT/bench_1d_$TAG.json" 2>&1
+      ok_or_stop $? bench1d; tail -1 "$OUT/bench_1d_$TAG.json" | cut -c1-900
+      timeout -k 10 300 python bench.py --dims 1 --size 67108864 --rate 8 --no-cpu-baseline --no-host-path > "$OUT/bench_1dL_$TAG.json" 2>&1
+      ok_or_stop $? bench1dL; tail -1 "$OUT/bench_1dL_$TAG.json" | cut -c1-900 ;;
     sizes)
       # throughput vs problem size (rounds of resident waves): 128^3 .. 512^3
       for sz in 128 192 256 384 512; do
