@@ -65,9 +65,9 @@ namespace cuzfp {
 // not form a read-modify-write chain through an accumulator and need no
 // flush branch; the coder's only serial state is `pos`.  Once W words are
 // filled the block is full; what the coder still produces (it finishes the
-// plane it is in, at most 128 bits + one straddled word) lands in the slack,
-// which the copy-out skips.
-constexpr uint32_t kSlackWords = 4;
+// pair of planes it is in: at most 2 x 128 bits + one straddled word) lands in
+// the slack, which the copy-out skips.
+constexpr uint32_t kSlackWords = 6;
 struct LdsOrWriter {
   uint64_t* p;          // the lane's W + kSlackWords words, zeroed
   uint32_t pos, lim;    // bits produced; 64 * W

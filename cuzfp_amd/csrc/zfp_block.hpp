@@ -490,22 +490,89 @@ ZFP_HD int uniform(int c) {
 #endif
 }
 
+// Group code of the not-yet-significant part r of a plane (see encode_plane):
+// G and its length L; dense is set (and G, L are not) when G would not fit 64
+// bits.
+template <int DIMS, typename PW>
+struct group_code {
+  uint64_t G;
+  unsigned L, adv;  // adv: how far n moves
+  bool dense;
+};
+
+// Two consecutive planes per step: both planes' codes are built before any is
+// written (plane B only needs n after plane A, one add), and their new ones
+// are spread by one merged loop, so the step has two independent chains and
+// half the loop overhead of plane-at-a-time coding.  Writers drop bits past
+// maxbits (the word writer into its slack), so plane B is written even when
+// plane A filled the block.
+template <int DIMS, typename PW, typename Writer>
+ZFP_HD void encode_plane_pair(PW xa, PW xb, unsigned& n, Writer& wr) {
+  constexpr unsigned N = 1u << (2 * DIMS);
+  constexpr unsigned SH = 8 * sizeof(PW) - 1;
+  const PW ra = n < N ? (PW)(xa >> (n & SH)) : (PW)0;
+  const unsigned ta = (unsigned)(sizeof(PW) == 8 ? __builtin_popcountll((uint64_t)ra) : __builtin_popcount((uint32_t)ra));
+  const unsigned pa = ra ? (unsigned)(8 * sizeof(PW) - 1) - (unsigned)(sizeof(PW) == 8 ? __builtin_clzll((uint64_t)ra) : __builtin_clz((uint32_t)ra)) : 0u;
+  const unsigned na = n + (ra ? pa + 1 : 0u);
+  const PW rb = na < N ? (PW)(xb >> (na & SH)) : (PW)0;
+  const unsigned tb = (unsigned)(sizeof(PW) == 8 ? __builtin_popcountll((uint64_t)rb) : __builtin_popcount((uint32_t)rb));
+  const unsigned pb = rb ? (unsigned)(8 * sizeof(PW) - 1) - (unsigned)(sizeof(PW) == 8 ? __builtin_clzll((uint64_t)rb) : __builtin_clz((uint32_t)rb)) : 0u;
+  const unsigned qa = pa + ta - 1, qb = pb + tb - 1;
+  if (__builtin_expect((ra && qa > 61) || (rb && qb > 61), 0)) {  // a dense plane
+    encode_plane<DIMS>(xa, n, wr);
+    encode_plane<DIMS>(xb, n, wr);
+    return;
+  }
+  uint64_t Fa = 0, Fb = 0;
+  PW a = ra, b = rb;
+  unsigned j = 0;
+  while (a | b) {  // F |= (j-th one) << j, both planes at once
+    const PW la = a & (PW)(0 - a), lb = b & (PW)(0 - b);
+    Fa |= (uint64_t)la << j;
+    Fb |= (uint64_t)lb << j;
+    a ^= la;
+    b ^= lb;
+    j++;
+  }
+  const bool lasta = pa + n == N - 1, lastb = pb + na == N - 1;
+  const unsigned La = ra ? qa + (lasta ? 1u : 3u) : (n < N ? 1u : 0u);
+  const unsigned Lb = rb ? qb + (lastb ? 1u : 3u) : (na < N ? 1u : 0u);
+  const uint64_t Ga = ra ? (1ull | (Fa << 1) | (Fa << 2)) & lowmask(lasta ? La : La - 1) : 0ull;
+  const uint64_t Gb = rb ? (1ull | (Fb << 1) | (Fb << 2)) & lowmask(lastb ? Lb : Lb - 1) : 0ull;
+  wr.put(xa & (PW)lowmask(n), n);
+  wr.put(Ga, La);
+  wr.put(xb & (PW)lowmask(na), na);
+  wr.put(Gb, Lb);
+  n = na + (rb ? pb + 1 : 0u);
+}
+
+// Planes 31 .. cmin of 32-bit half H, two at a time (an odd one left at the
+// bottom goes alone); false once the block is full.
+template <int H, typename UInt, int DIMS, typename Writer>
+ZFP_HD bool encode_half(const planes<UInt, DIMS>& P, unsigned& n, int cmin, Writer& wr) {
+  typedef typename plane_word<DIMS>::type PW;
+  int c = 31;
+  for (; c - 1 >= cmin; c -= 2) {
+    if (wr.full()) return false;
+    const int u = uniform(c);
+    encode_plane_pair<DIMS>((PW)P.template get<H>(u), (PW)P.template get<H>(u - 1), n, wr);
+  }
+  if (c >= cmin && c >= 0) {
+    if (wr.full()) return false;
+    encode_plane<DIMS>((PW)P.template get<H>(uniform(c)), n, wr);
+  }
+  return true;
+}
+
 template <typename UInt, int DIMS, typename Writer>
 ZFP_HD void encode_planes(const planes<UInt, DIMS>& P, unsigned maxprec, Writer& wr) {
-  typedef typename plane_word<DIMS>::type PW;
   constexpr int PREC = (int)sizeof(UInt) * 8;
   const int kmin = PREC > (int)maxprec ? PREC - (int)maxprec : 0;
   unsigned n = 0;
   if constexpr (PREC == 64) {
-    for (int c = 31; c >= 0 && c + 32 >= kmin; c--) {
-      if (wr.full()) return;
-      encode_plane<DIMS>((PW)P.template get<1>(uniform(c)), n, wr);
-    }
+    if (!encode_half<1>(P, n, kmin > 32 ? kmin - 32 : 0, wr)) return;
   }
-  for (int c = 31; c >= 0 && c >= kmin; c--) {
-    if (wr.full()) return;
-    encode_plane<DIMS>((PW)P.template get<0>(uniform(c)), n, wr);
-  }
+  encode_half<0>(P, n, kmin, wr);
 }
 
 // Decoder plane step (decode.c:288-321).
