@@ -56,6 +56,11 @@ __device__ __forceinline__ void stamp_real(int slot) {
 
 namespace cuzfp {
 
+// The plane decoder's chunk tables (zfp_block.hpp), generated at compile time;
+// each decode workgroup copies them to LDS.
+__device__ const ChunkLut g_chunk_lut = make_chunk_lut();
+constexpr size_t kChunkLutBytes = sizeof(ChunkLut);
+
 // ---------------------------------------------------------------------------
 // LDS bit writers / reader (one lane, one block)
 
@@ -122,7 +127,10 @@ struct LdsBitWriter {
   }
 };
 
-// Reader over the wave's LDS stream image.  It keeps the five dwords that
+// Reader over the lane's block in the wave's lane-interleaved LDS image
+// (dword j of the block at lds32[64 * j]; pos counts bits from the block's
+// start).  The table decoder reads its windows fresh per plane; the general
+// decoder (decode_plane) keeps the five dwords that
 // cover bits [pos, pos + 128) in registers: peek()/peek2() funnel them into
 // place with v_alignbit_b32, and skip() moves the bit offset and issues the
 // LDS reads for the new position at once.  The plane decoder skips as soon as
@@ -130,15 +138,32 @@ struct LdsBitWriter {
 // so those reads land while it still has work to do.
 struct LdsReader {
   const uint32_t* lds32;
+  const uint32_t* lut32;  // the workgroup's copy of the chunk tables
   uint32_t pos;
   uint32_t x0, x1, x2, x3, x4;
+  // table decoder: 64 bits at pos and 32 bits at pos + m, read fresh
+  __device__ __forceinline__ void windows(uint32_t m, uint64_t& w, uint32_t& g) const {
+    const uint32_t d = pos >> 5, q = pos + m, e = q >> 5;
+    const uint32_t* r = lds32 + d * 64;
+    const uint32_t* t = lds32 + e * 64;
+    const uint32_t a0 = r[0], a1 = r[64], a2 = r[128];
+    const uint32_t b0 = t[0], b1 = t[64];
+    w = (uint64_t)__builtin_amdgcn_alignbit(a1, a0, pos) |
+        ((uint64_t)__builtin_amdgcn_alignbit(a2, a1, pos) << 32);
+    g = __builtin_amdgcn_alignbit(b1, b0, q);
+  }
+  __device__ __forceinline__ uint32_t lut(uint32_t i) const { return lut32[i]; }
+  __device__ __forceinline__ void lut2(uint32_t i, uint32_t& a, uint32_t& b) const {
+    a = lut32[i];
+    b = lut32[i + (1u << kChunkBits)];
+  }
   __device__ __forceinline__ void load() {
-    const uint32_t d = pos >> 5;
-    x0 = lds32[d];
-    x1 = lds32[d + 1];
-    x2 = lds32[d + 2];
-    x3 = lds32[d + 3];
-    x4 = lds32[d + 4];
+    const uint32_t* r = lds32 + (pos >> 5) * 64;
+    x0 = r[0];
+    x1 = r[64];
+    x2 = r[128];
+    x3 = r[192];
+    x4 = r[256];
   }
   __device__ __forceinline__ void init(uint32_t bitpos) {
     pos = bitpos;
@@ -364,32 +389,61 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
                                                                       Scalar* __restrict__ data) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds_all[];
   constexpr int N = 1 << (2 * DIMS);
+  // chunk tables of the plane decoder: one copy per workgroup, after the
+  // waves' stream images, filled before any wave of the group can leave
+  uint32_t* lut = (uint32_t*)(lds_all + (size_t)(blockDim.x >> 6) * g.lds_words);
+  for (uint32_t i = threadIdx.x; i < (2u << kChunkBits) / 4; i += blockDim.x)
+    ((uint4*)lut)[i] = ((const uint4*)g_chunk_lut.e)[i];
+  __syncthreads();
   const uint32_t wig = threadIdx.x >> 6;
   const uint32_t wave = g.wave0 + blockIdx.x * (blockDim.x >> 6) + wig;
   if (wave >= g.wave_end) return;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t b = wave * kLanes + lane;
   uint64_t* lds = lds_all + (size_t)wig * g.lds_words;
-  const uint32_t nb = min((uint32_t)kLanes, g.nblocks - wave * kLanes);
-  const uint32_t nwords = (nb * g.maxbits + 63) >> 6;
-  const uint64_t* in = stream + (size_t)wave * g.maxbits;
-  if (g.vec_io) {
-    const uint32_t npairs = nwords >> 1;
-    for (uint32_t j = lane; j < npairs; j += kLanes) ((uint4*)lds)[j] = ((const uint4*)in)[j];
-    if ((nwords & 1) && lane == 0) lds[nwords - 1] = in[nwords - 1];
-  } else {
-    for (uint32_t j = lane; j < nwords; j += kLanes) lds[j] = in[j];
+  // Copy-in: each lane moves its own block into an LDS image stored
+  // lane-interleaved -- dword j of lane l at dword j*64 + l -- so the plane
+  // decoder's per-lane window reads hit 32 distinct banks whatever each lane's
+  // read position (a contiguous image puts lanes maxbits/32 dwords apart, up
+  // to 16 to a bank).  Rows D .. D+4 are zero slack for the reader.
+  const uint32_t D = (g.maxbits + 31) >> 5;  // dwords per block
+  uint32_t* L = (uint32_t*)lds + lane;
+  if (b < g.nblocks) {
+    const uint32_t* seg = (const uint32_t*)(stream + (size_t)wave * g.maxbits);
+    if ((g.maxbits & 127) == 0 && g.vec_io) {
+      const uint4* src = (const uint4*)(seg + lane * D);
+      for (uint32_t q = 0; q < D; q += 4) {
+        const uint4 v = src[q >> 2];
+        L[q * 64] = v.x;
+        L[(q + 1) * 64] = v.y;
+        L[(q + 2) * 64] = v.z;
+        L[(q + 3) * 64] = v.w;
+      }
+    } else {
+      // the block starts at bit lane*maxbits of the wave's segment; dwords
+      // past the segment's last one read as zero
+      const uint32_t nb = min((uint32_t)kLanes, g.nblocks - wave * kLanes);
+      const uint32_t lim = ((nb * g.maxbits + 63) >> 6) * 2;
+      const uint32_t s0 = lane * g.maxbits, d0 = s0 >> 5;
+      uint32_t prev = seg[d0];
+      for (uint32_t j = 0; j < D; j++) {
+        const uint32_t nxt = d0 + j + 1 < lim ? seg[d0 + j + 1] : 0u;
+        L[j * 64] = __builtin_amdgcn_alignbit(nxt, prev, s0);
+        prev = nxt;
+      }
+    }
   }
+  for (uint32_t j = D; j < D + 5; j++) L[j * 64] = 0;
   ZFP_STAMP_HWID();
   ZFP_STAMP_REAL(8);
   ZFP_STAMP(0);
-  if (lane < 6) lds[nwords + lane] = 0;  // reader look-ahead slack
   wave_lds_sync();
   ZFP_STAMP(5);
   if (b < g.nblocks) {
     LdsReader rd;
-    rd.lds32 = (const uint32_t*)lds;
-    rd.init(lane * g.maxbits);
+    rd.lds32 = L;
+    rd.lut32 = lut;
+    rd.init(0);
     Scalar f[N];
     decode_block<Scalar, DIMS>(f, g.maxbits, rd);
     scatter<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
@@ -402,9 +456,9 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
 // Launchers
 
 // waves per workgroup: as many as fit a workgroup's 64 KiB of LDS (up to 4)
-static inline uint32_t waves_per_group(uint32_t lds_words) {
+static inline uint32_t waves_per_group(uint32_t lds_words, size_t shared_bytes = 0) {
   uint32_t w = kWavesPerGroup;
-  while (w > 1 && (size_t)w * lds_words * 8 > 65536) w >>= 1;
+  while (w > 1 && (size_t)w * lds_words * 8 + shared_bytes > 65536) w >>= 1;
   return w;
 }
 
@@ -443,11 +497,10 @@ int launch_decode_t(const uint64_t* stream, const Geometry& g, bool fast, void* 
   gg.wave0 = wave0;
   gg.wave_end = wave0 + nwaves;
   gg.vec_io = (g.maxbits % 2 == 0) && ((uintptr_t)stream % 16 == 0);
-  gg.lds_words = g.maxbits + 6;  // + the reader's look-ahead slack
-  gg.lds_words += gg.lds_words & 1;  // keep every wave's image 16-byte aligned
-  const uint32_t wpg = waves_per_group(gg.lds_words);
+  gg.lds_words = ((g.maxbits + 31) / 32 + 5) * 32;  // (dwords per block + 5 slack rows) x 64 lanes
+  const uint32_t wpg = waves_per_group(gg.lds_words, kChunkLutBytes);
   const dim3 grid((nwaves + wpg - 1) / wpg), block(kLanes * wpg);
-  const size_t lds = (size_t)wpg * gg.lds_words * 8;
+  const size_t lds = (size_t)wpg * gg.lds_words * 8 + kChunkLutBytes;
   Scalar* d = (Scalar*)data;
   if (fast)
     hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, true>), grid, block, lds, st, stream, gg, d);

@@ -758,6 +758,118 @@ ZFP_HD PW decode_plane(unsigned& bits, unsigned& n, Reader& rd) {
   return x;
 }
 
+// ---------------------------------------------------------------------------
+// Table-driven plane decoder (the common case).
+//
+// A group code after its leading "1" test is a token string: "0" (a position
+// that stays zero) or "1g" (a new one, then the group test g; g = 0 ends the
+// code).  kChunkBits bits of it are parsed by one table lookup: the entry of
+// (state, chunk) -- state 1 meaning the chunk's first bit is the pending g of
+// a one that closed the previous chunk -- gives the ones it places (as a bit
+// pattern over the positions it covers), how many positions it covers, and,
+// if the code ends inside it, how many bits it used.  Two chunks are looked
+// up side by side (the second in both states), so one plane costs three table
+// reads and no loop.  The tables are generated at compile time from the token
+// grammar (decode.c:302-317 read the same grammar bit by bit).
+constexpr int kChunkBits = 10;
+constexpr uint32_t kChunkMask = (1u << kChunkBits) - 1;
+// entry: ones [0,10) | positions [10,14) | bits used [14,18) | state' bit 29 | end bit 31
+constexpr uint32_t kEntryState = 1u << 29, kEntryEnd = 1u << 31;
+
+constexpr uint32_t chunk_entry(unsigned state, uint32_t b) {
+  uint32_t ones = 0, pos = 0;
+  unsigned i = 0;
+  if (state) {  // the pending group test of the previous chunk's last one
+    i = 1;
+    if (!(b & 1u)) return kEntryEnd | (1u << 14);
+  }
+  while (i < (unsigned)kChunkBits) {
+    if (!((b >> i) & 1u)) {  // a position that stays zero
+      pos++;
+      i++;
+      continue;
+    }
+    ones |= 1u << pos;  // a new one
+    pos++;
+    i++;
+    if (i == (unsigned)kChunkBits)  // its group test is in the next chunk
+      return ones | (pos << 10) | ((unsigned)kChunkBits << 14) | kEntryState;
+    const bool more = (b >> i) & 1u;
+    i++;
+    if (!more) return ones | (pos << 10) | (i << 14) | kEntryEnd;
+  }
+  return ones | (pos << 10) | ((unsigned)kChunkBits << 14);
+}
+
+struct ChunkLut {
+  uint32_t e[2u << kChunkBits];  // [state][chunk]
+};
+constexpr ChunkLut make_chunk_lut() {
+  ChunkLut t{};
+  for (unsigned s = 0; s < 2; s++)
+    for (uint32_t b = 0; b <= kChunkMask; b++) t.e[(s << kChunkBits) | b] = chunk_entry(s, b);
+  return t;
+}
+
+// m = 0 .. 64 low bits set
+ZFP_HD uint64_t lowmask64(unsigned m) { return m ? ~0ull >> ((64u - m) & 63u) : 0ull; }
+
+// One plane by table lookup.  Reader: windows(m, w, g) gives the 64 stream
+// bits at the read position (w) and the 32 bits m further on (g);
+// lut(i) / lut2(i, a, b) read entries i (state 0) and i, i + 2^kChunkBits.
+// Returns the plane; `slow` is set, and nothing is consumed, for a plane the
+// tables cannot finish (a code longer than two chunks, one that runs into the
+// budget, or one that reaches position N-1, where the one is implied): the
+// caller decodes that plane again with decode_plane.
+template <int DIMS, typename PW, typename Reader>
+ZFP_HD PW decode_plane_lut(unsigned& bits, unsigned& n, Reader& rd, bool& slow) {
+  constexpr unsigned N = 1u << (2 * DIMS);
+  const unsigned m = umin(n, bits);
+  uint64_t w;
+  uint32_t g;
+  rd.windows(m, w, g);
+  PW x = (PW)(w & lowmask64(m));
+  const unsigned b1 = bits - m;                // budget after the verbatim bits
+  const bool gx = n < N && b1 != 0;            // a leading group test is read
+  const bool g0 = gx && (g & 1u);              // ... and it is a one
+  const uint32_t e1 = rd.lut((g >> 1) & kChunkMask);
+  uint32_t e2a, e2b;
+  rd.lut2((g >> (1 + kChunkBits)) & kChunkMask, e2a, e2b);
+  const uint32_t e2 = (e1 & kEntryState) ? e2b : e2a;
+  const bool end1 = (e1 & kEntryEnd) != 0;
+  const uint32_t p1 = (e1 >> 10) & 15u;
+  const uint32_t ones = end1 ? (e1 & kChunkMask) : (e1 & kChunkMask) | ((e2 & kChunkMask) << p1);
+  const uint32_t npos = end1 ? p1 : p1 + ((e2 >> 10) & 15u);
+  const uint32_t used = end1 ? (e1 >> 14) & 15u : (uint32_t)kChunkBits + ((e2 >> 14) & 15u);
+  const bool ended = end1 || (e2 & kEntryEnd) != 0;
+  const bool ok = ended && used + 1 <= b1 && n + npos <= N - 1;
+  slow = g0 && !ok;
+  const bool take = g0 && ok;
+  x |= (PW)(take ? ones : 0u) << (n & (8 * sizeof(PW) - 1));
+  n += take ? npos : 0u;
+  const unsigned adv = m + (gx ? 1u : 0u) + (take ? used : 0u);
+  rd.pos += adv;
+  bits -= adv;
+  return x;
+}
+
+// Plane loop: the table decoder for every lane, then, only when some lane of
+// the wave needs it, the general decoder for those lanes.
+template <int DIMS, typename PW, typename Reader>
+ZFP_HD PW decode_plane_any(unsigned& bits, unsigned& n, Reader& rd) {
+  const auto pos0 = rd.pos;
+  const unsigned n0 = n, bits0 = bits;
+  bool slow;
+  PW x = decode_plane_lut<DIMS, PW>(bits, n, rd, slow);
+  if (__builtin_expect(slow, 0)) {
+    rd.init(pos0);
+    n = n0;
+    bits = bits0;
+    x = decode_plane<DIMS, PW>(bits, n, rd);
+  }
+  return x;
+}
+
 template <typename UInt, int DIMS, typename Reader>
 ZFP_HD void decode_planes(planes<UInt, DIMS>& P, unsigned budget, unsigned maxprec, Reader& rd) {
   typedef typename plane_word<DIMS>::type PW;
@@ -768,12 +880,12 @@ ZFP_HD void decode_planes(planes<UInt, DIMS>& P, unsigned budget, unsigned maxpr
   if constexpr (PREC == 64) {
     for (int c = 31; c >= 0 && c + 32 >= kmin; c--) {
       if (!bits) return;
-      P.template set<1>(uniform(c), decode_plane<DIMS, PW>(bits, n, rd));
+      P.template set<1>(uniform(c), decode_plane_any<DIMS, PW>(bits, n, rd));
     }
   }
   for (int c = 31; c >= 0 && c >= kmin; c--) {
     if (!bits) return;
-    P.template set<0>(uniform(c), decode_plane<DIMS, PW>(bits, n, rd));
+    P.template set<0>(uniform(c), decode_plane_any<DIMS, PW>(bits, n, rd));
   }
 }
 

@@ -58,6 +58,23 @@ struct HostReader {
     pos -= 64;
   }
   void skip(unsigned n) { pos += n; }
+  void init(size_t p) { pos = p; }
+  // table decoder interface (see LdsReader in kernels.hpp)
+  void windows(unsigned m, uint64_t& w, uint32_t& g) {
+    w = peek();
+    pos += m;
+    g = (uint32_t)peek();
+    pos -= m;
+  }
+  static const cuzfp::ChunkLut& table() {
+    static const cuzfp::ChunkLut t = cuzfp::make_chunk_lut();
+    return t;
+  }
+  uint32_t lut(uint32_t i) const { return table().e[i]; }
+  void lut2(uint32_t i, uint32_t& a, uint32_t& b) const {
+    a = table().e[i];
+    b = table().e[i + (1u << cuzfp::kChunkBits)];
+  }
 };
 
 template <typename Scalar, int DIMS>

@@ -18,6 +18,11 @@ struct Rd {
   uint64_t peek() const { unsigned sh = pos & 63; size_t i = pos >> 6; return sh ? (w(i) >> sh) | (w(i + 1) << (64 - sh)) : w(i); }
   void peek2(uint64_t& a, uint64_t& b) { a = peek(); pos += 64; b = peek(); pos -= 64; }
   void skip(unsigned n) { pos += n; }
+  void init(size_t p) { pos = p; }
+  void windows(unsigned m, uint64_t& w, uint32_t& g) { w = peek(); pos += m; g = (uint32_t)peek(); pos -= m; }
+  static const cuzfp::ChunkLut& table() { static const cuzfp::ChunkLut t = cuzfp::make_chunk_lut(); return t; }
+  uint32_t lut(uint32_t i) const { return table().e[i]; }
+  void lut2(uint32_t i, uint32_t& a, uint32_t& b) const { a = table().e[i]; b = table().e[i + (1u << cuzfp::kChunkBits)]; }
 };
 struct Wr {
   uint64_t* s; size_t pos, end;
