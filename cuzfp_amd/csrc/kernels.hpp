@@ -60,6 +60,9 @@ namespace cuzfp {
 // each decode workgroup copies them to LDS.
 __device__ const ChunkLut g_chunk_lut = make_chunk_lut();
 constexpr size_t kChunkLutBytes = sizeof(ChunkLut);
+// ... and the plane coder's spread table (each encode workgroup copies it)
+__device__ const SpreadLut g_spread_lut = make_spread_lut();
+constexpr size_t kSpreadLutBytes = sizeof(SpreadLut);
 
 // ---------------------------------------------------------------------------
 // LDS bit writers / reader (one lane, one block)
@@ -74,15 +77,18 @@ constexpr size_t kChunkLutBytes = sizeof(ChunkLut);
 // the slack, which the copy-out skips.
 constexpr uint32_t kSlackWords = 6;
 struct LdsOrWriter {
-  uint64_t* p;          // the lane's W + kSlackWords words, zeroed
+  uint64_t* p;          // the lane's column: word j at p[64 j], W + kSlackWords words, zeroed
+  const uint32_t* lut;  // the workgroup's spread table
   uint32_t pos, lim;    // bits produced; 64 * W
   __device__ __forceinline__ bool full() const { return pos >= lim; }
   __device__ __forceinline__ void put(uint64_t v, unsigned n) {  // v < 2^n
     const uint32_t w = pos >> 6, sh = pos & 63;
-    atomicOr((unsigned long long*)&p[w], (unsigned long long)(v << sh));
-    atomicOr((unsigned long long*)&p[w + 1], (unsigned long long)((v >> 1) >> (63 - sh)));
+    uint64_t* q = p + w * 64;
+    atomicOr((unsigned long long*)&q[0], (unsigned long long)(v << sh));
+    atomicOr((unsigned long long*)&q[64], (unsigned long long)((v >> 1) >> (63 - sh)));
     pos += n;
   }
+  __device__ __forceinline__ uint32_t spread(uint32_t b) const { return lut[b]; }
   __device__ __forceinline__ void zero_bit() { pos++; }
   __device__ __forceinline__ void finish() {}
 };
@@ -92,8 +98,10 @@ struct LdsOrWriter {
 // the first and last words of a lane's range are shared with its neighbours.
 struct LdsBitWriter {
   uint64_t* lds;
+  const uint32_t* lut;     // the workgroup's spread table
   uint32_t pos, end, cnt;  // pos: stream offset of acc's bit 0
   uint64_t acc;
+  __device__ __forceinline__ uint32_t spread(uint32_t b) const { return lut[b]; }
   __device__ __forceinline__ bool full() const { return pos + cnt >= end; }
   __device__ __forceinline__ void emit(uint64_t v) {
     if (pos >= end) return;  // bits past maxbits are dropped
@@ -325,6 +333,12 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
                                                                       uint64_t* __restrict__ stream) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds_all[];
   constexpr int N = 1 << (2 * DIMS);
+  // spread table of the plane coder: one copy per workgroup, after the waves'
+  // stream images, filled before any wave of the group can leave
+  uint32_t* lut = (uint32_t*)(lds_all + (size_t)(blockDim.x >> 6) * g.lds_words);
+  for (uint32_t i = threadIdx.x; i < 256 / 4; i += blockDim.x)
+    ((uint4*)lut)[i] = ((const uint4*)g_spread_lut.e)[i];
+  __syncthreads();
   const uint32_t wig = threadIdx.x >> 6;  // wave in workgroup
   const uint32_t wave = g.wave0 + blockIdx.x * (blockDim.x >> 6) + wig;
   if (wave >= g.wave_end) return;
@@ -338,17 +352,20 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
     for (uint32_t j = lane; j < g.maxbits + 2; j += kLanes) lds[j] = 0;
     wave_lds_sync();
   }
-  const uint32_t W = g.maxbits >> 6, WS = W + kSlackWords;  // ALIGNED: lane stride in words
+  // ALIGNED: the wave's image is lane-interleaved, word j of lane l's block at
+  // lds[64 j + l] (conflict-free ds_or_b64 whatever each lane's bit position),
+  // W words per block plus kSlackWords rows
+  const uint32_t W = g.maxbits >> 6;
   if (b < g.nblocks) {
     Scalar f[N];
     gather<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
     if constexpr (ALIGNED) {
-      uint64_t* mine = lds + (size_t)lane * WS;
-      for (uint32_t j = 0; j < WS; j++) mine[j] = 0;  // own words only: no barrier
-      LdsOrWriter wr{mine, 0, 64 * W};
+      uint64_t* mine = lds + lane;
+      for (uint32_t j = 0; j < W + kSlackWords; j++) mine[j * 64] = 0;  // own column: no barrier
+      LdsOrWriter wr{mine, lut, 0, 64 * W};
       encode_block<Scalar, DIMS>(f, g.maxbits, wr);
     } else {
-      LdsBitWriter wr{lds, lane * g.maxbits, (lane + 1) * g.maxbits, 0, 0};
+      LdsBitWriter wr{lds, lut, lane * g.maxbits, (lane + 1) * g.maxbits, 0, 0};
       encode_block<Scalar, DIMS>(f, g.maxbits, wr);
     }
   }
@@ -357,18 +374,20 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
   const uint32_t nwords = (nb * g.maxbits + 63) >> 6;
   uint64_t* out = stream + (size_t)wave * g.maxbits;
   if constexpr (ALIGNED) {
-    // stream word o = word j of lane l's block, l = o / W (exact in float for
-    // o < 8000, W <= 125: (o + 1/2) / W stays >= 0.5/W away from integers)
-    const float rw = 1.0f / (float)W;
-    if (g.vec_io && !(W & 1)) {  // 16-byte pairs, never split across lanes
-      for (uint32_t o = 2 * lane; o < nwords; o += 2 * kLanes) {
-        const uint32_t l = (uint32_t)(((float)o + 0.5f) * rw), j = o - l * W;
-        *(uint4*)&out[o] = *(const uint4*)&lds[l * WS + j];
-      }
-    } else {
-      for (uint32_t o = lane; o < nwords; o += kLanes) {
-        const uint32_t l = (uint32_t)(((float)o + 0.5f) * rw), j = o - l * W;
-        out[o] = lds[l * WS + j];
+    // each lane stores its own block: W words at out + lane * W
+    if (b < g.nblocks) {
+      const uint64_t* mine = lds + lane;
+      uint64_t* dst = out + (size_t)lane * W;
+      if (g.vec_io && !(W & 1)) {
+        for (uint32_t j = 0; j < W; j += 2) {
+          uint4 v;
+          const uint64_t a0 = mine[j * 64], a1 = mine[(j + 1) * 64];
+          __builtin_memcpy(&v.x, &a0, 8);
+          __builtin_memcpy(&v.z, &a1, 8);
+          *(uint4*)&dst[j] = v;
+        }
+      } else {
+        for (uint32_t j = 0; j < W; j++) dst[j] = mine[j * 64];
       }
     }
   } else if (g.vec_io) {  // 16-byte aligned segment
@@ -472,10 +491,11 @@ int launch_encode_t(const void* data, const Geometry& g, bool fast, uint64_t* st
   gg.lds_words = g.maxbits + kLanes * kSlackWords;  // + per-lane slack
   // the word-aligned writer pads each lane with slack words; very large maxbits
   // (whose padded image would pass 64 KiB of LDS) take the general writer
-  const bool aligned = (g.maxbits & 63) == 0 && gg.lds_words * 8 <= 65536;
-  const uint32_t wpg = waves_per_group(gg.lds_words);
+  const bool aligned = (g.maxbits & 63) == 0 && gg.lds_words * 8 + kSpreadLutBytes <= 65536;
+  if (!aligned) gg.lds_words = g.maxbits + 2;
+  const uint32_t wpg = waves_per_group(gg.lds_words, kSpreadLutBytes);
   const dim3 grid((nwaves + wpg - 1) / wpg), block(kLanes * wpg);
-  const size_t lds = (size_t)wpg * gg.lds_words * 8;
+  const size_t lds = (size_t)wpg * gg.lds_words * 8 + kSpreadLutBytes;
   const Scalar* d = (const Scalar*)data;
   if (fast && aligned)
     hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, true, true>), grid, block, lds, st, d, gg, stream);

@@ -546,6 +546,64 @@ ZFP_HD void encode_plane_pair(PW xa, PW xb, unsigned& n, Writer& wr) {
   n = na + (rb ? pb + 1 : 0u);
 }
 
+// Table-driven plane step (the common case).  The group code of the plane's
+// not-yet-significant part r is "1", then for every position up to r's top
+// one its bit, each one followed by a "1" group test -- i.e. r with every one
+// doubled -- with the top one's test flipped to the closing "0" (or, when the
+// top one sits at position N-1, that one and its test omitted: it is implied).
+// The doubling is read from a 256-entry table per byte of r (Writer::spread),
+// so a plane costs two table reads and no loop over its ones.  Returns false,
+// writing nothing, when r has bits beyond its low 16 (a dense plane; the caller
+// codes it with encode_plane).
+constexpr uint32_t spread_entry(uint32_t b) {
+  uint32_t e = 0, p = 0;
+  for (int i = 0; i < 8; i++) {
+    if ((b >> i) & 1u) {
+      e |= 3u << p;
+      p += 2;
+    } else {
+      p += 1;
+    }
+  }
+  return e;
+}
+struct SpreadLut {
+  uint32_t e[256];
+};
+constexpr SpreadLut make_spread_lut() {
+  SpreadLut t{};
+  for (uint32_t b = 0; b < 256; b++) t.e[b] = spread_entry(b);
+  return t;
+}
+
+template <int DIMS, typename PW, typename Writer>
+ZFP_HD bool encode_plane_lut(PW x, unsigned& n, Writer& wr) {
+  constexpr unsigned N = 1u << (2 * DIMS);
+  const uint64_t xx = (uint64_t)x;
+  const uint64_t r = n < N ? xx >> (n & 63) : 0ull;
+  if (r >> 16) return false;
+  const uint64_t v = xx ^ (r << (n & 63));  // the verbatim bits x & lowmask(n)
+  const uint32_t rl = (uint32_t)r, b0 = rl & 0xffu, b1 = rl >> 8;
+  const uint32_t p0 = (uint32_t)__builtin_popcount(b0);
+  const uint32_t t = p0 + (uint32_t)__builtin_popcount(b1);
+  const uint32_t E = wr.spread(b0) | (wr.spread(b1) << (8 + p0));   // r, ones doubled
+  const uint32_t bl = rl ? 32u - (uint32_t)__builtin_clz(rl) : 0u;  // positions covered
+  const uint32_t L = bl + t;                                          // bits of E
+  const bool implied = n + bl == N;                                   // (needs r != 0)
+  uint64_t G = ((uint64_t)E << 1) | 1ull;
+  G ^= implied ? 3ull << ((L - 1) & 63) : 1ull << (L & 63);
+  const uint32_t glen = rl ? (implied ? L - 1 : L + 1) : (n < N ? 1u : 0u);
+  wr.put(v, n);
+  wr.put(rl ? G : 0ull, glen);
+  n += bl;
+  return true;
+}
+
+template <int DIMS, typename PW, typename Writer>
+ZFP_HD void encode_plane_any(PW x, unsigned& n, Writer& wr) {
+  if (__builtin_expect(!encode_plane_lut<DIMS>(x, n, wr), 0)) encode_plane<DIMS>(x, n, wr);
+}
+
 // Planes 31 .. cmin of 32-bit half H, two at a time (an odd one left at the
 // bottom goes alone); false once the block is full.
 template <int H, typename UInt, int DIMS, typename Writer>
@@ -555,11 +613,12 @@ ZFP_HD bool encode_half(const planes<UInt, DIMS>& P, unsigned& n, int cmin, Writ
   for (; c - 1 >= cmin; c -= 2) {
     if (wr.full()) return false;
     const int u = uniform(c);
-    encode_plane_pair<DIMS>((PW)P.template get<H>(u), (PW)P.template get<H>(u - 1), n, wr);
+    encode_plane_any<DIMS>((PW)P.template get<H>(u), n, wr);
+    encode_plane_any<DIMS>((PW)P.template get<H>(u - 1), n, wr);
   }
   if (c >= cmin && c >= 0) {
     if (wr.full()) return false;
-    encode_plane<DIMS>((PW)P.template get<H>(uniform(c)), n, wr);
+    encode_plane_any<DIMS>((PW)P.template get<H>(uniform(c)), n, wr);
   }
   return true;
 }

@@ -39,6 +39,10 @@ struct HostWriter {
     if (pos < end) pos++;
   }
   void finish() {}
+  uint32_t spread(uint32_t b) const {
+    static const cuzfp::SpreadLut t = cuzfp::make_spread_lut();
+    return t.e[b];
+  }
 };
 
 struct HostReader {

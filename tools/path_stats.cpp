@@ -35,6 +35,7 @@ struct Wr {
   }
   void zero_bit() { if (pos < end) pos++; }
   void finish() {}
+  uint32_t spread(uint32_t b) const { static const cuzfp::SpreadLut t = cuzfp::make_spread_lut(); return t.e[b]; }
 };
 
 int main(int argc, char** argv) {

@@ -19,6 +19,7 @@ struct Wr {
   }
   void zero_bit() { if (pos < end) pos++; }
   void finish() {}
+  uint32_t spread(uint32_t b) const { static const cuzfp::SpreadLut t = cuzfp::make_spread_lut(); return t.e[b]; }
 };
 
 enum { NOGRP, G0, END, IMPLIED, BUDGET, NCASE };
