@@ -333,18 +333,17 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
                                                                       uint64_t* __restrict__ stream) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds_all[];
   constexpr int N = 1 << (2 * DIMS);
-  // spread table of the plane coder: one copy per workgroup, after the waves'
-  // stream images, filled before any wave of the group can leave
-  uint32_t* lut = (uint32_t*)(lds_all + (size_t)(blockDim.x >> 6) * g.lds_words);
-  for (uint32_t i = threadIdx.x; i < 256 / 4; i += blockDim.x)
-    ((uint4*)lut)[i] = ((const uint4*)g_spread_lut.e)[i];
-  __syncthreads();
   const uint32_t wig = threadIdx.x >> 6;  // wave in workgroup
   const uint32_t wave = g.wave0 + blockIdx.x * (blockDim.x >> 6) + wig;
   if (wave >= g.wave_end) return;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t b = wave * kLanes + lane;
   uint64_t* lds = lds_all + (size_t)wig * g.lds_words;
+  // the plane coder's spread table, one copy per wave (after the group's
+  // stream images): its load is issued first so that storing it waits only
+  // for it, not for the block's gathers
+  const uint4 spread16 = ((const uint4*)g_spread_lut.e)[lane];
+  uint32_t* lut = (uint32_t*)(lds_all + (size_t)(blockDim.x >> 6) * g.lds_words) + wig * 256;
   ZFP_STAMP_HWID();
   ZFP_STAMP_REAL(8);
   ZFP_STAMP(0);
@@ -356,15 +355,18 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
   // lds[64 j + l] (conflict-free ds_or_b64 whatever each lane's bit position),
   // W words per block plus kSlackWords rows
   const uint32_t W = g.maxbits >> 6;
+  Scalar f[N];
+  if (b < g.nblocks) gather<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
+  ((uint4*)lut)[lane] = spread16;  // every lane: the table is the wave's
   if (b < g.nblocks) {
-    Scalar f[N];
-    gather<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
     if constexpr (ALIGNED) {
       uint64_t* mine = lds + lane;
-      for (uint32_t j = 0; j < W + kSlackWords; j++) mine[j * 64] = 0;  // own column: no barrier
+      for (uint32_t j = 0; j < W + kSlackWords; j++) mine[j * 64] = 0;  // own column
+      wave_lds_sync();  // the wave's table
       LdsOrWriter wr{mine, lut, 0, 64 * W};
       encode_block<Scalar, DIMS>(f, g.maxbits, wr);
     } else {
+      wave_lds_sync();  // the wave's table
       LdsBitWriter wr{lds, lut, lane * g.maxbits, (lane + 1) * g.maxbits, 0, 0};
       encode_block<Scalar, DIMS>(f, g.maxbits, wr);
     }
@@ -408,30 +410,46 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
                                                                       Scalar* __restrict__ data) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds_all[];
   constexpr int N = 1 << (2 * DIMS);
-  // chunk tables of the plane decoder: one copy per workgroup, after the
-  // waves' stream images, filled before any wave of the group can leave
-  uint32_t* lut = (uint32_t*)(lds_all + (size_t)(blockDim.x >> 6) * g.lds_words);
-  for (uint32_t i = threadIdx.x; i < (2u << kChunkBits) / 4; i += blockDim.x)
-    ((uint4*)lut)[i] = ((const uint4*)g_chunk_lut.e)[i];
-  __syncthreads();
   const uint32_t wig = threadIdx.x >> 6;
   const uint32_t wave = g.wave0 + blockIdx.x * (blockDim.x >> 6) + wig;
-  if (wave >= g.wave_end) return;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t b = wave * kLanes + lane;
+  const bool live = wave < g.wave_end && b < g.nblocks;
   uint64_t* lds = lds_all + (size_t)wig * g.lds_words;
   // Copy-in: each lane moves its own block into an LDS image stored
   // lane-interleaved -- dword j of lane l at dword j*64 + l -- so the plane
   // decoder's per-lane window reads hit 32 distinct banks whatever each lane's
   // read position (a contiguous image puts lanes maxbits/32 dwords apart, up
-  // to 16 to a bank).  Rows D .. D+4 are zero slack for the reader.
+  // to 16 to a bank).  Rows D .. D+4 are zero slack for the reader.  The
+  // block's loads are issued first, then the workgroup's copy of the chunk
+  // tables, so both latencies overlap before the one barrier.
   const uint32_t D = (g.maxbits + 31) >> 5;  // dwords per block
   uint32_t* L = (uint32_t*)lds + lane;
-  if (b < g.nblocks) {
-    const uint32_t* seg = (const uint32_t*)(stream + (size_t)wave * g.maxbits);
-    if ((g.maxbits & 127) == 0 && g.vec_io) {
+  const uint32_t* seg = (const uint32_t*)(stream + (size_t)wave * g.maxbits);
+  const bool vec = (g.maxbits & 127) == 0 && g.vec_io;
+  constexpr uint32_t kHeld = 8;  // 16-byte pieces held in registers (maxbits <= 1024)
+  uint4 held[kHeld];
+  if (live && vec) {
+    const uint4* src = (const uint4*)(seg + lane * D);
+#pragma unroll
+    for (uint32_t q = 0; q < kHeld; q++)
+      if (4 * q < D) held[q] = src[q];
+  }
+  uint32_t* lut = (uint32_t*)(lds_all + (size_t)(blockDim.x >> 6) * g.lds_words);
+  for (uint32_t i = threadIdx.x; i < (2u << kChunkBits) / 4; i += blockDim.x)
+    ((uint4*)lut)[i] = ((const uint4*)g_chunk_lut.e)[i];
+  if (live) {
+    if (vec) {
+#pragma unroll
+      for (uint32_t q = 0; q < kHeld; q++)
+        if (4 * q < D) {
+          L[(4 * q) * 64] = held[q].x;
+          L[(4 * q + 1) * 64] = held[q].y;
+          L[(4 * q + 2) * 64] = held[q].z;
+          L[(4 * q + 3) * 64] = held[q].w;
+        }
       const uint4* src = (const uint4*)(seg + lane * D);
-      for (uint32_t q = 0; q < D; q += 4) {
+      for (uint32_t q = 4 * kHeld; q < D; q += 4) {  // larger blocks
         const uint4 v = src[q >> 2];
         L[q * 64] = v.x;
         L[(q + 1) * 64] = v.y;
@@ -452,7 +470,10 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
       }
     }
   }
-  for (uint32_t j = D; j < D + 5; j++) L[j * 64] = 0;
+  if (wave < g.wave_end)
+    for (uint32_t j = D; j < D + 5; j++) L[j * 64] = 0;
+  __syncthreads();
+  if (wave >= g.wave_end) return;
   ZFP_STAMP_HWID();
   ZFP_STAMP_REAL(8);
   ZFP_STAMP(0);
@@ -493,9 +514,9 @@ int launch_encode_t(const void* data, const Geometry& g, bool fast, uint64_t* st
   // (whose padded image would pass 64 KiB of LDS) take the general writer
   const bool aligned = (g.maxbits & 63) == 0 && gg.lds_words * 8 + kSpreadLutBytes <= 65536;
   if (!aligned) gg.lds_words = g.maxbits + 2;
-  const uint32_t wpg = waves_per_group(gg.lds_words, kSpreadLutBytes);
+  const uint32_t wpg = waves_per_group(gg.lds_words + kSpreadLutBytes / 8);
   const dim3 grid((nwaves + wpg - 1) / wpg), block(kLanes * wpg);
-  const size_t lds = (size_t)wpg * gg.lds_words * 8 + kSpreadLutBytes;
+  const size_t lds = (size_t)wpg * (gg.lds_words * 8 + kSpreadLutBytes);
   const Scalar* d = (const Scalar*)data;
   if (fast && aligned)
     hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, true, true>), grid, block, lds, st, d, gg, stream);
