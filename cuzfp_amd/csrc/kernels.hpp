@@ -149,11 +149,21 @@ struct LdsReader {
   const uint32_t* lut32;  // the workgroup's copy of the chunk tables
   uint32_t pos;
   uint32_t x0, x1, x2, x3, x4;
+  // byte address of the row holding bit p: lds32 + 256 * (p >> 5), in two
+  // instructions (the compiler's form of the same expression takes three)
+  typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+  __device__ __forceinline__ lds_u32* row(uint32_t p) const {
+    uint32_t a;
+    asm("v_lshl_add_u32 %0, %1, 8, %2"
+        : "=v"(a)
+        : "v"(p >> 5), "v"((uint32_t)(uintptr_t)(lds_u32*)lds32));
+    return (lds_u32*)(uintptr_t)a;
+  }
   // table decoder: 64 bits at pos and 32 bits at pos + m, read fresh
   __device__ __forceinline__ void windows(uint32_t m, uint64_t& w, uint32_t& g) const {
-    const uint32_t d = pos >> 5, q = pos + m, e = q >> 5;
-    const uint32_t* r = lds32 + d * 64;
-    const uint32_t* t = lds32 + e * 64;
+    const uint32_t q = pos + m;
+    lds_u32* r = row(pos);
+    lds_u32* t = row(q);
     const uint32_t a0 = r[0], a1 = r[64], a2 = r[128];
     const uint32_t b0 = t[0], b1 = t[64];
     w = (uint64_t)__builtin_amdgcn_alignbit(a1, a0, pos) |
@@ -436,7 +446,7 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
       if (4 * q < D) held[q] = src[q];
   }
   uint32_t* lut = (uint32_t*)(lds_all + (size_t)(blockDim.x >> 6) * g.lds_words);
-  for (uint32_t i = threadIdx.x; i < (2u << kChunkBits) / 4; i += blockDim.x)
+  for (uint32_t i = threadIdx.x; i < sizeof(ChunkLut) / 16; i += blockDim.x)
     ((uint4*)lut)[i] = ((const uint4*)g_chunk_lut.e)[i];
   if (live) {
     if (vec) {

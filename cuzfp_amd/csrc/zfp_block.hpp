@@ -835,10 +835,16 @@ constexpr uint32_t kChunkMask = (1u << kChunkBits) - 1;
 // entry: ones [0,10) | positions [10,14) | bits used [14,18) | state' bit 29 | end bit 31
 constexpr uint32_t kEntryState = 1u << 29, kEntryEnd = 1u << 31;
 
+// state 0: at a token boundary; 1: the first bit is the pending group test of
+// a one that closed the previous chunk; 2: the first bit is the plane's
+// leading group test (0 = no new ones in this plane)
 constexpr uint32_t chunk_entry(unsigned state, uint32_t b) {
   uint32_t ones = 0, pos = 0;
   unsigned i = 0;
-  if (state) {  // the pending group test of the previous chunk's last one
+  if (state == 2) {
+    i = 1;
+    if (!(b & 1u)) return kEntryEnd | (1u << 14);
+  } else if (state == 1) {
     i = 1;
     if (!(b & 1u)) return kEntryEnd | (1u << 14);
   }
@@ -861,11 +867,11 @@ constexpr uint32_t chunk_entry(unsigned state, uint32_t b) {
 }
 
 struct ChunkLut {
-  uint32_t e[2u << kChunkBits];  // [state][chunk]
+  uint32_t e[3u << kChunkBits];  // [state][chunk]
 };
 constexpr ChunkLut make_chunk_lut() {
   ChunkLut t{};
-  for (unsigned s = 0; s < 2; s++)
+  for (unsigned s = 0; s < 3; s++)
     for (uint32_t b = 0; b <= kChunkMask; b++) t.e[(s << kChunkBits) | b] = chunk_entry(s, b);
   return t;
 }
@@ -890,23 +896,27 @@ ZFP_HD PW decode_plane_lut(unsigned& bits, unsigned& n, Reader& rd, bool& slow) 
   PW x = (PW)(w & lowmask64(m));
   const unsigned b1 = bits - m;                // budget after the verbatim bits
   const bool gx = n < N && b1 != 0;            // a leading group test is read
-  const bool g0 = gx && (g & 1u);              // ... and it is a one
-  const uint32_t e1 = rd.lut((g >> 1) & kChunkMask);
+  // chunk 1 starts at the group test (table state 2), chunk 2 in either state
+  const uint32_t e1 = rd.lut(((uint32_t)2 << kChunkBits) | (g & kChunkMask));
   uint32_t e2a, e2b;
-  rd.lut2((g >> (1 + kChunkBits)) & kChunkMask, e2a, e2b);
+  rd.lut2((g >> kChunkBits) & kChunkMask, e2a, e2b);
   const uint32_t e2 = (e1 & kEntryState) ? e2b : e2a;
   const bool end1 = (e1 & kEntryEnd) != 0;
   const uint32_t p1 = (e1 >> 10) & 15u;
-  const uint32_t ones = end1 ? (e1 & kChunkMask) : (e1 & kChunkMask) | ((e2 & kChunkMask) << p1);
-  const uint32_t npos = end1 ? p1 : p1 + ((e2 >> 10) & 15u);
-  const uint32_t used = end1 ? (e1 >> 14) & 15u : (uint32_t)kChunkBits + ((e2 >> 14) & 15u);
-  const bool ended = end1 || (e2 & kEntryEnd) != 0;
-  const bool ok = ended && used + 1 <= b1 && n + npos <= N - 1;
-  slow = g0 && !ok;
-  const bool take = g0 && ok;
+  // both combinations computed, then selected (no branch on end1)
+  const uint32_t ones2 = (e1 & kChunkMask) | ((e2 & kChunkMask) << p1);
+  const uint32_t npos2 = p1 + ((e2 >> 10) & 15u);
+  const uint32_t used2 = (uint32_t)kChunkBits + ((e2 >> 14) & 15u);
+  const uint32_t ones = end1 ? (e1 & kChunkMask) : ones2;
+  const uint32_t npos = end1 ? p1 : npos2;
+  const uint32_t used = end1 ? (e1 >> 14) & 15u : used2;
+  const bool ended = ((e1 | e2) & kEntryEnd) != 0;
+  const bool ok = ended && used <= b1 && n + npos <= N - 1;
+  slow = gx && !ok;
+  const bool take = gx && ok;
   x |= (PW)(take ? ones : 0u) << (n & (8 * sizeof(PW) - 1));
   n += take ? npos : 0u;
-  const unsigned adv = m + (gx ? 1u : 0u) + (take ? used : 0u);
+  const unsigned adv = m + (take ? used : 0u);
   rd.pos += adv;
   bits -= adv;
   return x;
@@ -929,23 +939,33 @@ ZFP_HD PW decode_plane_any(unsigned& bits, unsigned& n, Reader& rd) {
   return x;
 }
 
+// Planes 31 .. cmin of 32-bit half H, two per loop trip.
+template <int H, typename UInt, int DIMS, typename Reader>
+ZFP_HD void decode_half(planes<UInt, DIMS>& P, unsigned& bits, unsigned& n, int cmin, Reader& rd) {
+  typedef typename plane_word<DIMS>::type PW;
+  int c = 31;
+  for (; c - 1 >= cmin; c -= 2) {
+    if (!bits) return;
+    const PW xa = decode_plane_any<DIMS, PW>(bits, n, rd);
+    const PW xb = decode_plane_any<DIMS, PW>(bits, n, rd);
+    const int u = uniform(c);
+    P.template set<H>(u, xa);
+    P.template set<H>(u - 1, xb);
+  }
+  if (c >= cmin && c >= 0 && bits) P.template set<H>(uniform(c), decode_plane_any<DIMS, PW>(bits, n, rd));
+}
+
 template <typename UInt, int DIMS, typename Reader>
 ZFP_HD void decode_planes(planes<UInt, DIMS>& P, unsigned budget, unsigned maxprec, Reader& rd) {
-  typedef typename plane_word<DIMS>::type PW;
   constexpr int PREC = (int)sizeof(UInt) * 8;
   const int kmin = PREC > (int)maxprec ? PREC - (int)maxprec : 0;
   unsigned bits = budget, n = 0;
   P.zero();
   if constexpr (PREC == 64) {
-    for (int c = 31; c >= 0 && c + 32 >= kmin; c--) {
-      if (!bits) return;
-      P.template set<1>(uniform(c), decode_plane_any<DIMS, PW>(bits, n, rd));
-    }
+    decode_half<1>(P, bits, n, kmin > 32 ? kmin - 32 : 0, rd);
+    if (kmin >= 32) return;
   }
-  for (int c = 31; c >= 0 && c >= kmin; c--) {
-    if (!bits) return;
-    P.template set<0>(uniform(c), decode_plane_any<DIMS, PW>(bits, n, rd));
-  }
+  decode_half<0>(P, bits, n, kmin, rd);
 }
 
 // ---------------------------------------------------------------------------
