@@ -353,6 +353,7 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
   // stream images): its load is issued first so that storing it waits only
   // for it, not for the block's gathers
   const uint4 spread16 = ((const uint4*)g_spread_lut.e)[lane];
+  __builtin_amdgcn_s_setprio(3);  // lowered through the plane loop (progress_priority)
   uint32_t* lut = (uint32_t*)(lds_all + (size_t)(blockDim.x >> 6) * g.lds_words) + wig * 256;
   ZFP_STAMP_HWID();
   ZFP_STAMP_REAL(8);
@@ -381,6 +382,7 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
       encode_block<Scalar, DIMS>(f, g.maxbits, wr);
     }
   }
+  __builtin_amdgcn_s_setprio(3);  // a wave out of the coder stores at once
   wave_lds_sync();
   const uint32_t nb = min((uint32_t)kLanes, g.nblocks - wave * kLanes);
   const uint32_t nwords = (nb * g.maxbits + 63) >> 6;
@@ -484,6 +486,7 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
     for (uint32_t j = D; j < D + 5; j++) L[j * 64] = 0;
   __syncthreads();
   if (wave >= g.wave_end) return;
+  __builtin_amdgcn_s_setprio(3);  // lowered through the plane loop (progress_priority)
   ZFP_STAMP_HWID();
   ZFP_STAMP_REAL(8);
   ZFP_STAMP(0);
@@ -496,6 +499,7 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
     rd.init(0);
     Scalar f[N];
     decode_block<Scalar, DIMS>(f, g.maxbits, rd);
+    __builtin_amdgcn_s_setprio(3);  // a wave out of the coder stores at once
     scatter<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
   }
   ZFP_STAMP(6);

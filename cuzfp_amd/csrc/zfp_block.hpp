@@ -490,6 +490,26 @@ ZFP_HD int uniform(int c) {
 #endif
 }
 
+// Wave priority from progress through the plane loop (c: the wave-uniform
+// plane number, counting down): a wave that is further along yields issue
+// slots to the other waves of its SIMD, so the SIMD's waves move through the
+// coder together instead of oldest-first (which leaves the last wave running
+// alone at the end, at a fraction of the SIMD's issue rate).
+#ifndef CUZFP_PRIO_T2  // plane numbers (odd: the loops step by two) where the priority drops
+#define CUZFP_PRIO_T2 21
+#define CUZFP_PRIO_T1 13
+#define CUZFP_PRIO_T0 5
+#endif
+ZFP_HD void progress_priority(int c) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(CUZFP_NO_PRIO)
+  if (c == CUZFP_PRIO_T2) __builtin_amdgcn_s_setprio(2);
+  else if (c == CUZFP_PRIO_T1) __builtin_amdgcn_s_setprio(1);
+  else if (c == CUZFP_PRIO_T0) __builtin_amdgcn_s_setprio(0);
+#else
+  (void)c;
+#endif
+}
+
 // Group code of the not-yet-significant part r of a plane (see encode_plane):
 // G and its length L; dense is set (and G, L are not) when G would not fit 64
 // bits.
@@ -613,6 +633,7 @@ ZFP_HD bool encode_half(const planes<UInt, DIMS>& P, unsigned& n, int cmin, Writ
   for (; c - 1 >= cmin; c -= 2) {
     if (wr.full()) return false;
     const int u = uniform(c);
+    progress_priority(u);
     encode_plane_any<DIMS>((PW)P.template get<H>(u), n, wr);
     encode_plane_any<DIMS>((PW)P.template get<H>(u - 1), n, wr);
   }
@@ -946,6 +967,7 @@ ZFP_HD void decode_half(planes<UInt, DIMS>& P, unsigned& bits, unsigned& n, int 
   int c = 31;
   for (; c - 1 >= cmin; c -= 2) {
     if (!bits) return;
+    progress_priority(uniform(c));
     const PW xa = decode_plane_any<DIMS, PW>(bits, n, rd);
     const PW xb = decode_plane_any<DIMS, PW>(bits, n, rd);
     const int u = uniform(c);
