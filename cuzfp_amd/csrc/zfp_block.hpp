@@ -932,12 +932,20 @@ ZFP_HD PW decode_plane_lut(unsigned& bits, unsigned& n, Reader& rd, bool& slow) 
   const uint32_t npos = end1 ? p1 : npos2;
   const uint32_t used = end1 ? (e1 >> 14) & 15u : used2;
   const bool ended = ((e1 | e2) & kEntryEnd) != 0;
-  const bool ok = ended && used <= b1 && n + npos <= N - 1;
+  // The stream reads as zeros past the block's last bit (the kernels and the
+  // host reader guarantee it) and the budget always ends there, so a code
+  // whose last one is the budget's last bit ends here one bit past the budget
+  // (its zero group test is not in the stream): the reference keeps that one
+  // and reads no more (decode.c:302-317).  Any other code the budget cuts
+  // short takes the general decoder.  (Decoding those here too costs the
+  // common case more than it saves.)
+  const bool ok = ended && used <= b1 + 1 && n + npos <= N - 1;
   slow = gx && !ok;
   const bool take = gx && ok;
-  x |= (PW)(take ? ones : 0u) << (n & (8 * sizeof(PW) - 1));
-  n += take ? npos : 0u;
-  const unsigned adv = m + (take ? used : 0u);
+  const uint32_t ones_f = ones, npos_f = npos, used_f = umin(used, b1);
+  x |= (PW)(take ? ones_f : 0u) << (n & (8 * sizeof(PW) - 1));
+  n += take ? npos_f : 0u;
+  const unsigned adv = m + (take ? used_f : 0u);
   rd.pos += adv;
   bits -= adv;
   return x;

@@ -49,11 +49,14 @@ struct HostReader {
   const uint64_t* s;
   size_t words;
   size_t pos;
+  size_t end;  // the block's last bit + 1: the stream reads as zeros from there (as on the GPU)
   uint64_t word(size_t i) const { return i < words ? s[i] : 0; }
   uint64_t peek() const {
+    if (pos >= end) return 0;
     const unsigned sh = pos & 63;
     const size_t w = pos >> 6;
-    return sh ? (word(w) >> sh) | (word(w + 1) << (64 - sh)) : word(w);
+    const uint64_t v = sh ? (word(w) >> sh) | (word(w + 1) << (64 - sh)) : word(w);
+    return end - pos < 64 ? v & cuzfp::lowmask((unsigned)(end - pos)) : v;
   }
   void peek2(uint64_t& a, uint64_t& b) {
     a = peek();
@@ -114,7 +117,7 @@ size_t run(bool enc, unsigned nx, unsigned ny, unsigned nz, long long sx, long l
       HostWriter wr{stream, b * (size_t)maxbits, (b + 1) * (size_t)maxbits};
       cuzfp::encode_block<Scalar, DIMS>(f, maxbits, wr);
     } else {
-      HostReader rd{stream, words, b * (size_t)maxbits};
+      HostReader rd{stream, words, b * (size_t)maxbits, (b + 1) * (size_t)maxbits};
       cuzfp::decode_block<Scalar, DIMS>(f, maxbits, rd);
       for (int i = 0; i < N; i++)
         if (valid[i]) data[off[i]] = f[i];
@@ -160,3 +163,52 @@ int emu_decompress(int type, unsigned nx, unsigned ny, unsigned nz, long long sx
 }
 
 }  // extern "C"
+
+// Differential fuzz of one plane step: the table decoder (decode_plane_any, the
+// kernels' path) against the general decoder (decode_plane, itself checked
+// against the oracle) from random states -- n, budget, stream bits of varied
+// density -- over a window that reads as zeros past the budget, as the
+// kernels' does.  Returns the number of mismatching (x, n, bits, pos) results.
+extern "C" long long emu_fuzz_plane(unsigned long long seed, long long trials, int dims) {
+  uint64_t st = seed;
+  auto rnd = [&]() {
+    st += 0x9e3779b97f4a7c15ull;
+    uint64_t z = st;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+  };
+  const unsigned N = 1u << (2 * dims);
+  long long bad = 0;
+  for (long long t = 0; t < trials; t++) {
+    uint64_t buf[6] = {0, 0, 0, 0, 0, 0};
+    const unsigned dens = (unsigned)(rnd() % 9);  // 0..8 -> one-bit probability dens/8 (0: structured)
+    for (int i = 0; i < 4; i++) {
+      uint64_t v = 0;
+      if (dens == 0) {
+        v = rnd() & rnd() & rnd();
+      } else {
+        for (int b = 0; b < 64; b++) v |= (uint64_t)((rnd() & 7u) < dens) << b;
+      }
+      buf[i] = v;
+    }
+    const unsigned n0 = (unsigned)(rnd() % (N + 1));
+    const unsigned bits0 = 1u + (unsigned)(rnd() % 160);
+    const size_t end = bits0;  // the budget ends where the block does
+    HostReader ra{buf, 6, 0, end}, rb{buf, 6, 0, end};
+    unsigned na = n0, ba = bits0, nb = n0, bb = bits0;
+    uint64_t xa, xb;
+    if (dims == 3) {
+      xa = cuzfp::decode_plane_any<3, uint64_t>(ba, na, ra);
+      xb = cuzfp::decode_plane<3, uint64_t>(bb, nb, rb);
+    } else if (dims == 2) {
+      xa = cuzfp::decode_plane_any<2, uint32_t>(ba, na, ra);
+      xb = cuzfp::decode_plane<2, uint32_t>(bb, nb, rb);
+    } else {
+      xa = cuzfp::decode_plane_any<1, uint32_t>(ba, na, ra);
+      xb = cuzfp::decode_plane<1, uint32_t>(bb, nb, rb);
+    }
+    if (xa != xb || na != nb || ba != bb || ra.pos != rb.pos) bad++;
+  }
+  return bad;
+}

@@ -143,3 +143,32 @@ def test_emulation_random_streams(emu, restatement, dims, dtype):
         want = restatement.decompress(s, shape, dtype, mb)
         got = emu_decompress(emu, s, shape, dtype, mb)
         assert np.array_equal(got.view(np.uint8), want.view(np.uint8)), (shape, mb, density)
+
+
+@pytest.mark.parametrize("dims", [1, 2, 3])
+def test_emulation_budget_cuts(emu, restatement, dims):
+    """Encoder output at every rate 1..32 (so the budget ends at every offset
+    of the table decoder's window), smooth, noisy and rough fields: the table
+    decoder's budget-cut and position-63 cases against the oracle."""
+    from cuzfp_amd.datagen import polynomial_field, splitmix_uniform
+    shape = {1: (4096,), 2: (64, 64), 3: (16, 16, 32)}[dims]
+    rng = np.random.default_rng(11 + dims)
+    fields = [polynomial_field(shape, np.float32), splitmix_uniform(shape, np.float32),
+              (polynomial_field(shape, np.float32) + 1e-3 * rng.standard_normal(shape)).astype(np.float32)]
+    for a in fields:
+        for rate in range(1, 33):
+            mb = restatement.rate_to_maxbits(rate, a.dtype, dims)
+            s = restatement.compress(a, mb)
+            assert np.array_equal(emu_compress(emu, a, mb), s), rate
+            got = emu_decompress(emu, s, a.shape, a.dtype, mb)
+            assert np.array_equal(got.view(np.uint8), restatement.decompress(s, a.shape, a.dtype, mb).view(np.uint8)), rate
+
+
+@pytest.mark.parametrize("dims", [1, 2, 3])
+def test_table_plane_decoder_fuzz(emu, dims):
+    """One plane step from random decoder states (n, budget, stream bits of
+    every density, the stream zero past the budget): the table decoder the
+    kernels run must equal the general decoder bit for bit."""
+    emu.emu_fuzz_plane.restype = ctypes.c_longlong
+    emu.emu_fuzz_plane.argtypes = [ctypes.c_ulonglong, ctypes.c_longlong, ctypes.c_int]
+    assert emu.emu_fuzz_plane(1234 + dims, 2_000_000, dims) == 0
