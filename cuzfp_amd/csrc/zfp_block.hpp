@@ -140,9 +140,21 @@ template <int DIMS, typename UInt, int... I>
 ZFP_HD void permute_fwd(const UInt* q, UInt* u, UInt nb, seq<I...>) {
   ((u[I] = (q[pidx<DIMS, I>::value] + nb) ^ nb), ...);
 }
+// (u ^ nb) - nb: one v_xad_u32 ((a ^ b) + c) for 32-bit words on the device
+ZFP_HD uint32_t from_negabinary(uint32_t u, uint32_t nb) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t r;
+  asm("v_xad_u32 %0, %1, %2, %3" : "=v"(r) : "v"(u), "s"(nb), "v"(0u - nb));  // one SGPR per VOP3
+  return r;
+#else
+  return (u ^ nb) - nb;
+#endif
+}
+ZFP_HD uint64_t from_negabinary(uint64_t u, uint64_t nb) { return (u ^ nb) - nb; }
+
 template <int DIMS, typename UInt, int... I>
 ZFP_HD void permute_inv(const UInt* u, UInt* q, UInt nb, seq<I...>) {
-  ((q[pidx<DIMS, I>::value] = (u[I] ^ nb) - nb), ...);
+  ((q[pidx<DIMS, I>::value] = from_negabinary(u[I], nb)), ...);
 }
 
 // precision() (codec1.c:8-11, codec2.c:131-136, codec3.c:92-97): planes coded
@@ -1092,7 +1104,32 @@ ZFP_HD void encode_block(const Scalar* f, unsigned maxbits, Writer& wr) {
     // oracle/zfp_oracle.c.
     const Scalar s = (Scalar)fp<Scalar>::pow2(T::prec - 2 - emax);
 #if defined(__HIP_DEVICE_COMPILE__)
+    // Fast path: in a block of finite values with a finite scale, |y| < 2^30
+    // (max |x| < 2^emax), so v_cvt_i32_f32's truncation is the x86 cast and
+    // the product pairs go through v_pk_mul_f32.  The block is finite when the
+    // sum of its values is (a NaN or inf makes the sum so; an overflowing sum
+    // of finite values only sends the block down the exact path below).
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    bool fast = false;
     if constexpr (sizeof(Scalar) == 4 && N % 2 == 0) {
+      f2 acc = {(float)f[0], (float)f[1]};
+#pragma unroll
+      for (int i = 2; i < N; i += 2) acc += f2{(float)f[i], (float)f[i + 1]};
+      fast = emax >= -97 && __builtin_isfinite(acc.x + acc.y);
+    }
+    if constexpr (sizeof(Scalar) == 4 && N % 2 == 0) {
+      if (fast) {
+        const f2 ss = {(float)s, (float)s};
+#pragma unroll
+        for (int i = 0; i < N; i += 2) {
+          const f2 y = f2{(float)f[i], (float)f[i + 1]} * ss;
+          q[i] = (UInt)(int32_t)y.x;  // v_cvt_i32_f32 (|y| < 2^30 here)
+          q[i + 1] = (UInt)(int32_t)y.y;
+        }
+      }
+    }
+    if (fast) {
+    } else if constexpr (sizeof(Scalar) == 4 && N % 2 == 0) {
       // Two values per statement, in place (tied operands), so the quantised
       // block reuses the input registers instead of doubling the block's
       // register footprint.  Each compare result is read >= 2 instructions
@@ -1211,8 +1248,23 @@ ZFP_HD void decode_block(Scalar* f, unsigned maxbits, Reader& rd) {
   ZFP_STAMP(3);
   if constexpr (!T::is_int) {
     const Scalar s = (Scalar)fp<Scalar>::pow2(emax - (T::prec - 2));
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (sizeof(Scalar) == 4 && N % 2 == 0) {
+      // two values per v_pk_mul_f32 (the same IEEE product as v_mul_f32)
+      typedef float f2 __attribute__((ext_vector_type(2)));
+      const f2 ss = {(float)s, (float)s};
 #pragma unroll
-    for (int i = 0; i < N; i++) f[i] = (Scalar)(s * (Scalar)(Int)q[i]);
+      for (int i = 0; i < N; i += 2) {
+        const f2 v = f2{(float)(Int)q[i], (float)(Int)q[i + 1]} * ss;
+        f[i] = (Scalar)v.x;
+        f[i + 1] = (Scalar)v.y;
+      }
+    } else
+#endif
+    {
+#pragma unroll
+      for (int i = 0; i < N; i++) f[i] = (Scalar)(s * (Scalar)(Int)q[i]);
+    }
   } else {
 #pragma unroll
     for (int i = 0; i < N; i++) f[i] = (Scalar)(Int)q[i];
