@@ -514,9 +514,13 @@ ZFP_HD int uniform(int c) {
 #endif
 ZFP_HD void progress_priority(int c) {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(CUZFP_NO_PRIO)
-  if (c == CUZFP_PRIO_T2) __builtin_amdgcn_s_setprio(2);
-  else if (c == CUZFP_PRIO_T1) __builtin_amdgcn_s_setprio(1);
-  else if (c == CUZFP_PRIO_T0) __builtin_amdgcn_s_setprio(0);
+  // one bit test on the common path (a compare cascade costs ~20 SALU a trip)
+  constexpr uint32_t kAt = (1u << CUZFP_PRIO_T2) | (1u << CUZFP_PRIO_T1) | (1u << CUZFP_PRIO_T0);
+  if (__builtin_expect((kAt >> (c & 31)) & 1u, 0)) {
+    if (c == CUZFP_PRIO_T2) __builtin_amdgcn_s_setprio(2);
+    else if (c == CUZFP_PRIO_T1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+  }
 #else
   (void)c;
 #endif
@@ -608,25 +612,52 @@ constexpr SpreadLut make_spread_lut() {
   return t;
 }
 
+// bit length of x < 2^24 (0 for 0): the exponent of (float)x, which frexp
+// gives as x in [2^(e-1), 2^e) -- two instructions, no zero test
+ZFP_HD uint32_t bitlen16(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t e;  // (the compiler's own u32 -> f32 form is the exact 64-bit one: 8 instructions)
+  asm("v_cvt_f32_u32 %0, %1\n\tv_frexp_exp_i32_f32 %0, %0" : "=&v"(e) : "v"(x));
+  return e;
+#else
+  return x ? 32u - (uint32_t)__builtin_clz(x) : 0u;
+#endif
+}
+
+// v << s as one v_lshlrev_b64: the compiler otherwise turns x ^ ((x >> n) << n)
+// into a mask with a zero-count guard (seven instructions)
+ZFP_HD uint64_t shl64(uint64_t v, uint32_t s) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint64_t r;
+  asm("v_lshlrev_b64 %0, %1, %2" : "=v"(r) : "v"(s), "v"(v));
+  return r;
+#else
+  return v << (s & 63);
+#endif
+}
+
 template <int DIMS, typename PW, typename Writer>
 ZFP_HD bool encode_plane_lut(PW x, unsigned& n, Writer& wr) {
   constexpr unsigned N = 1u << (2 * DIMS);
   const uint64_t xx = (uint64_t)x;
   const uint64_t r = n < N ? xx >> (n & 63) : 0ull;
   if (r >> 16) return false;
-  const uint64_t v = xx ^ (r << (n & 63));  // the verbatim bits x & lowmask(n)
+  const uint64_t v = xx ^ shl64(r, n);  // the verbatim bits x & lowmask(n)
   const uint32_t rl = (uint32_t)r, b0 = rl & 0xffu, b1 = rl >> 8;
   const uint32_t p0 = (uint32_t)__builtin_popcount(b0);
   const uint32_t t = p0 + (uint32_t)__builtin_popcount(b1);
   const uint32_t E = wr.spread(b0) | (wr.spread(b1) << (8 + p0));   // r, ones doubled
-  const uint32_t bl = rl ? 32u - (uint32_t)__builtin_clz(rl) : 0u;  // positions covered
+  const uint32_t nz = rl ? 1u : 0u;                                   // any new ones
+  const uint32_t bl = bitlen16(rl);                                   // positions covered
   const uint32_t L = bl + t;                                          // bits of E
-  const bool implied = n + bl == N;                                   // (needs r != 0)
-  uint64_t G = ((uint64_t)E << 1) | 1ull;
-  G ^= implied ? 3ull << ((L - 1) & 63) : 1ull << (L & 63);
-  const uint32_t glen = rl ? (implied ? L - 1 : L + 1) : (n < N ? 1u : 0u);
+  const uint32_t imp = n + bl == N ? nz : 0u;                         // top one at N-1: implied
+  // branch-free: "1" + E with the top one's test flipped to the closing "0"
+  // (imp: that one and its test dropped instead); no new ones: G = 0 and the
+  // single "0" test (none once n = N)
+  const uint64_t G = (((uint64_t)E << 1) | nz) ^ ((uint64_t)(nz | (imp << 1)) << ((L - imp) & 63));
+  const uint32_t glen = L + (n < N ? 1u : 0u) - 2u * imp;
   wr.put(v, n);
-  wr.put(rl ? G : 0ull, glen);
+  wr.put(G, glen);
   n += bl;
   return true;
 }
