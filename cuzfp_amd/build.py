@@ -3,6 +3,8 @@
 Outputs (git-ignored, shipped to the GPU box with the repo snapshot):
   cuzfp_amd/lib/libcuzfp_hip.so  -- kernels + the C-ABI of include/cuzfp_hip.h
   cuzfp_amd/lib/libcuZFP.so      -- the reference's C++ surface (include/cuZFP.h)
+  cuzfp_amd/bin/cuda_zfp         -- the reference's CLI (src/utils/cuda_zfp.cpp) on libcuZFP.so
+  cuzfp_amd/bin/data_gen         -- the reference's test-data generator (src/utils/data_gen.cpp)
 """
 from __future__ import annotations
 
@@ -15,6 +17,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "lib")
+BIN = os.path.join(HERE, "bin")
+CLI = os.path.join(HERE, "cli")
 OBJ = os.path.join(ROOT, "build", "obj")
 INC = os.path.join(ROOT, "include")
 
@@ -68,7 +72,16 @@ def build(verbose: bool = False, jobs: int | None = None) -> dict:
                        os.path.join(INC, "zfp_structs.h")]):
         _run([HIPCC, "-O2", "-std=c++17", "-fPIC", "-shared", f"-I{INC}", "-o", cpp_so, cpp_src,
               f"-L{LIB}", "-lcuzfp_hip", "-Wl,-rpath,$ORIGIN"])
-    return {"hip": hip_so, "cpp": cpp_so}
+    os.makedirs(BIN, exist_ok=True)
+    cli = os.path.join(BIN, "cuda_zfp")
+    if _newer(cli, [os.path.join(CLI, "cuda_zfp.cpp"), cpp_so, os.path.join(INC, "cuZFP.h"),
+                    os.path.join(INC, "zfp_structs.h")]):
+        _run(["g++", "-O2", "-std=c++17", "-Wall", "-Wno-unused-function", f"-I{INC}", "-o", cli,
+              os.path.join(CLI, "cuda_zfp.cpp"), f"-L{LIB}", "-lcuZFP", "-Wl,-rpath,$ORIGIN/../lib"])
+    gen = os.path.join(BIN, "data_gen")
+    if _newer(gen, [os.path.join(CLI, "data_gen.cpp")]):
+        _run(["g++", "-O2", "-std=c++17", "-Wall", "-o", gen, os.path.join(CLI, "data_gen.cpp")])
+    return {"hip": hip_so, "cpp": cpp_so, "cli": cli, "data_gen": gen}
 
 
 if __name__ == "__main__":
