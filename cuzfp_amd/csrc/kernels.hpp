@@ -91,6 +91,9 @@ struct LdsOrWriter {
   __device__ __forceinline__ uint32_t spread(uint32_t b) const { return lut[b]; }
   __device__ __forceinline__ void zero_bit() { pos++; }
   __device__ __forceinline__ void finish() {}
+  // a full lane keeps stepping with its wave: restart it at the first slack
+  // row each plane, so its (discarded) pieces stay within rows W .. W + 3
+  __device__ __forceinline__ void settle() { pos = pos < lim ? pos : lim; }
 };
 
 // general maxbits: the lane's bits are [pos0, end) of the wave's segment;
@@ -133,6 +136,7 @@ struct LdsBitWriter {
   __device__ __forceinline__ void finish() {
     if (cnt && pos < end) emit(acc);
   }
+  __device__ __forceinline__ void settle() {}  // emit() drops bits past maxbits
 };
 
 // Reader over the lane's block in the wave's lane-interleaved LDS image
@@ -170,10 +174,20 @@ struct LdsReader {
         ((uint64_t)__builtin_amdgcn_alignbit(a2, a1, pos) << 32);
     g = __builtin_amdgcn_alignbit(b1, b0, q);
   }
-  __device__ __forceinline__ uint32_t lut(uint32_t i) const { return lut32[i]; }
-  __device__ __forceinline__ void lut2(uint32_t i, uint32_t& a, uint32_t& b) const {
-    a = lut32[i];
-    b = lut32[i + (1u << kChunkBits)];
+  // table decoder: entry (2, g's chunk 1) -- or the no-group entry -- and
+  // entries (0, chunk 2), (1, chunk 2); addresses in two instructions each
+  // (the compiler's forms take three)
+  __device__ __forceinline__ void chunks(uint32_t g, bool group, uint32_t& e1, uint32_t& e2a,
+                                         uint32_t& e2b) const {
+    const uint32_t base = (uint32_t)(uintptr_t)(lds_u32*)lut32;
+    const uint32_t c1 = group ? (g & kChunkMask) : kNoGroupEntry - (2u << kChunkBits);
+    uint32_t a1, c2, a2;
+    asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a1) : "v"(c1), "s"(base));
+    asm("v_bfe_u32 %0, %1, %2, %2" : "=v"(c2) : "v"(g), "i"(kChunkBits));
+    asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a2) : "v"(c2), "s"(base));
+    e1 = ((lds_u32*)(uintptr_t)a1)[2u << kChunkBits];
+    e2a = ((lds_u32*)(uintptr_t)a2)[0];
+    e2b = ((lds_u32*)(uintptr_t)a2)[1u << kChunkBits];
   }
   __device__ __forceinline__ void load() {
     const uint32_t* r = lds32 + (pos >> 5) * 64;
@@ -366,6 +380,12 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
   // lds[64 j + l] (conflict-free ds_or_b64 whatever each lane's bit position),
   // W words per block plus kSlackWords rows
   const uint32_t W = g.maxbits >> 6;
+#ifdef CUZFP_STAGGER
+  {  // experiment: the k-th quarter of the grid (a SIMD's k-th wave) loads k steps later
+    const uint32_t rank = blockIdx.x * 4 / gridDim.x;
+    for (uint32_t r = 0; r < rank; r++) __builtin_amdgcn_s_sleep(CUZFP_STAGGER);
+  }
+#endif
   Scalar f[N];
   if (b < g.nblocks) gather<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
   ((uint4*)lut)[lane] = spread16;  // every lane: the table is the wave's

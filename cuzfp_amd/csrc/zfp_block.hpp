@@ -502,23 +502,50 @@ ZFP_HD int uniform(int c) {
 #endif
 }
 
+// Plane-loop exit: the loops run while any lane of the wave still has budget,
+// and a finished lane's steps are no-ops (the decoder's consume nothing and
+// deposit zeros; the encoder's write into the lane's slack, see
+// Writer::settle).  Exiting per lane instead costs ~15 exec-mask instructions
+// a loop trip.  On the host a "wave" is one lane.
+ZFP_HD bool any_lane(bool p) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(CUZFP_LANE_EXIT)
+  return __builtin_amdgcn_ballot_w64(p) != 0;
+#else
+  return p;
+#endif
+}
+
 // Wave priority from progress through the plane loop (c: the wave-uniform
 // plane number, counting down): a wave that is further along yields issue
 // slots to the other waves of its SIMD, so the SIMD's waves move through the
 // coder together instead of oldest-first (which leaves the last wave running
 // alone at the end, at a fraction of the SIMD's issue rate).
+//
+// The encoder drops to 2, 1, 0 at planes 21, 13, 5; its copy-out runs at 3
+// again.  The decoder drops to 2 and 1 at planes 21 and 11 and to 0 only after
+// its plane loop, so a wave in the inverse transform (a quarter of a decode
+// wave's instructions) yields to every wave still decoding planes: with the
+// transform at the loop's last level the oldest wave of each SIMD finished
+// ~8 us before the youngest, which then ran alone.
 #ifndef CUZFP_PRIO_T2  // plane numbers (odd: the loops step by two) where the priority drops
 #define CUZFP_PRIO_T2 21
 #define CUZFP_PRIO_T1 13
 #define CUZFP_PRIO_T0 5
 #endif
+#ifndef CUZFP_DPRIO_T2
+#define CUZFP_DPRIO_T2 21
+#define CUZFP_DPRIO_T1 11
+#define CUZFP_DPRIO_T0 (-1)
+#define CUZFP_DPRIO_AFTER 0
+#endif
+template <int T2, int T1, int T0>
 ZFP_HD void progress_priority(int c) {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(CUZFP_NO_PRIO)
   // one bit test on the common path (a compare cascade costs ~20 SALU a trip)
-  constexpr uint32_t kAt = (1u << CUZFP_PRIO_T2) | (1u << CUZFP_PRIO_T1) | (1u << CUZFP_PRIO_T0);
+  constexpr uint32_t kAt = (1u << T2) | (1u << T1) | (T0 >= 0 ? 1u << (T0 & 31) : 0u);
   if (__builtin_expect((kAt >> (c & 31)) & 1u, 0)) {
-    if (c == CUZFP_PRIO_T2) __builtin_amdgcn_s_setprio(2);
-    else if (c == CUZFP_PRIO_T1) __builtin_amdgcn_s_setprio(1);
+    if (c == T2) __builtin_amdgcn_s_setprio(2);
+    else if (c == T1) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
   }
 #else
@@ -674,14 +701,16 @@ ZFP_HD bool encode_half(const planes<UInt, DIMS>& P, unsigned& n, int cmin, Writ
   typedef typename plane_word<DIMS>::type PW;
   int c = 31;
   for (; c - 1 >= cmin; c -= 2) {
-    if (wr.full()) return false;
+    if (!any_lane(!wr.full())) return false;
+    wr.settle();
     const int u = uniform(c);
-    progress_priority(u);
+    progress_priority<CUZFP_PRIO_T2, CUZFP_PRIO_T1, CUZFP_PRIO_T0>(u);
     encode_plane_any<DIMS>((PW)P.template get<H>(u), n, wr);
     encode_plane_any<DIMS>((PW)P.template get<H>(u - 1), n, wr);
   }
   if (c >= cmin && c >= 0) {
-    if (wr.full()) return false;
+    if (!any_lane(!wr.full())) return false;
+    wr.settle();
     encode_plane_any<DIMS>((PW)P.template get<H>(uniform(c)), n, wr);
   }
   return true;
@@ -896,21 +925,37 @@ ZFP_HD PW decode_plane(unsigned& bits, unsigned& n, Reader& rd) {
 // grammar (decode.c:302-317 read the same grammar bit by bit).
 constexpr int kChunkBits = 10;
 constexpr uint32_t kChunkMask = (1u << kChunkBits) - 1;
-// entry: ones [0,10) | positions [10,14) | bits used [14,18) | state' bit 29 | end bit 31
-constexpr uint32_t kEntryState = 1u << 29, kEntryEnd = 1u << 31;
+// entry: bits used U [0,14) | 0 | ones [15,25) | positions covered [26,31) |
+// exit state bit 31.  The fields have room for the sum of two entries (ones
+// < 2^11, positions <= 20 < 2^5, U wraps into the zero bit), so one add
+// combines chunk 1 and chunk 2.  U also says whether the code ended, by a
+// marker M = 2^13 (larger than any budget, maxbits <= 8000): a chunk-1 entry
+// that did not end carries M, a chunk-2 entry that did end carries M too, so
+// the sum's U holds M (mod 2^14) exactly when the code has not ended -- and
+// one compare against the budget rejects both a code running past the budget
+// and one longer than two chunks.
+constexpr unsigned kOnesShift = 15, kPosShift = 26;
+constexpr uint32_t kUsedMask = (1u << 14) - 1, kNotEnded = 1u << 13;
+constexpr uint32_t kEntryState = 1u << 31;
+// a last entry, for planes with no group part (n = N): ended, nothing used
+constexpr uint32_t kNoGroupEntry = 3u << kChunkBits;
+
+constexpr uint32_t pack_entry(uint32_t ones, uint32_t pos, uint32_t used, uint32_t flags) {
+  return (ones << kOnesShift) | (pos << kPosShift) | used | flags;
+}
 
 // state 0: at a token boundary; 1: the first bit is the pending group test of
 // a one that closed the previous chunk; 2: the first bit is the plane's
 // leading group test (0 = no new ones in this plane)
 constexpr uint32_t chunk_entry(unsigned state, uint32_t b) {
+  // the marker: state 2 (chunk 1) entries that do not end, state 0/1 (chunk 2)
+  // entries that do
+  const uint32_t mark_end = state == 2 ? 0u : kNotEnded, mark_open = state == 2 ? kNotEnded : 0u;
   uint32_t ones = 0, pos = 0;
   unsigned i = 0;
-  if (state == 2) {
+  if (state == 2 || state == 1) {
     i = 1;
-    if (!(b & 1u)) return kEntryEnd | (1u << 14);
-  } else if (state == 1) {
-    i = 1;
-    if (!(b & 1u)) return kEntryEnd | (1u << 14);
+    if (!(b & 1u)) return pack_entry(0, 0, 1 + mark_end, 0);
   }
   while (i < (unsigned)kChunkBits) {
     if (!((b >> i) & 1u)) {  // a position that stays zero
@@ -922,34 +967,50 @@ constexpr uint32_t chunk_entry(unsigned state, uint32_t b) {
     pos++;
     i++;
     if (i == (unsigned)kChunkBits)  // its group test is in the next chunk
-      return ones | (pos << 10) | ((unsigned)kChunkBits << 14) | kEntryState;
+      return pack_entry(ones, pos, kChunkBits + mark_open, kEntryState);
     const bool more = (b >> i) & 1u;
     i++;
-    if (!more) return ones | (pos << 10) | (i << 14) | kEntryEnd;
+    if (!more) return pack_entry(ones, pos, i + mark_end, 0);
   }
-  return ones | (pos << 10) | ((unsigned)kChunkBits << 14);
+  return pack_entry(ones, pos, kChunkBits + mark_open, 0);
 }
 
 struct ChunkLut {
-  uint32_t e[3u << kChunkBits];  // [state][chunk]
+  uint32_t e[(3u << kChunkBits) + 4];  // [state][chunk], the no-group entry, padding to 16 B
 };
 constexpr ChunkLut make_chunk_lut() {
   ChunkLut t{};
   for (unsigned s = 0; s < 3; s++)
     for (uint32_t b = 0; b <= kChunkMask; b++) t.e[(s << kChunkBits) | b] = chunk_entry(s, b);
+  t.e[kNoGroupEntry] = pack_entry(0, 0, 0, 0);
   return t;
 }
 
 // m = 0 .. 64 low bits set
 ZFP_HD uint64_t lowmask64(unsigned m) { return m ? ~0ull >> ((64u - m) & 63u) : 0ull; }
 
+// v when bit 13 of e is set, else 0 (v_bfe_i32 + v_and_b32)
+ZFP_HD uint32_t keep_if_bit13(uint32_t v, uint32_t e) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t m;
+  asm("v_bfe_i32 %0, %1, 13, 1" : "=v"(m) : "v"(e));
+  return v & m;
+#else
+  return (e >> 13) & 1u ? v : 0u;
+#endif
+}
+
 // One plane by table lookup.  Reader: windows(m, w, g) gives the 64 stream
 // bits at the read position (w) and the 32 bits m further on (g);
-// lut(i) / lut2(i, a, b) read entries i (state 0) and i, i + 2^kChunkBits.
-// Returns the plane; `slow` is set, and nothing is consumed, for a plane the
-// tables cannot finish (a code longer than two chunks, one that runs into the
-// budget, or one that reaches position N-1, where the one is implied): the
-// caller decodes that plane again with decode_plane.
+// chunks(g, group, e1, e2a, e2b) reads the entry of g's first chunk in state 2
+// (the no-group entry when !group) and of its second chunk in states 0 and 1.
+// Sets `slow` for a plane the tables cannot finish (a code longer than two
+// chunks, one that runs into the budget, or one that reaches position N-1,
+// where the one is implied); the caller then discards this step's result and
+// state and decodes the plane again with decode_plane.  So nothing here is
+// gated on `slow`: a lane out of budget (b1 = 0) reads zeros past its block
+// (its group test reads as a "0" it does not consume), and a plane with no
+// group part (n = N) looks up the empty entry.
 template <int DIMS, typename PW, typename Reader>
 ZFP_HD PW decode_plane_lut(unsigned& bits, unsigned& n, Reader& rd, bool& slow) {
   constexpr unsigned N = 1u << (2 * DIMS);
@@ -957,38 +1018,32 @@ ZFP_HD PW decode_plane_lut(unsigned& bits, unsigned& n, Reader& rd, bool& slow) 
   uint64_t w;
   uint32_t g;
   rd.windows(m, w, g);
-  PW x = (PW)(w & lowmask64(m));
+  const uint64_t vmask = lowmask64(m);
   const unsigned b1 = bits - m;                // budget after the verbatim bits
-  const bool gx = n < N && b1 != 0;            // a leading group test is read
-  // chunk 1 starts at the group test (table state 2), chunk 2 in either state
-  const uint32_t e1 = rd.lut(((uint32_t)2 << kChunkBits) | (g & kChunkMask));
-  uint32_t e2a, e2b;
-  rd.lut2((g >> kChunkBits) & kChunkMask, e2a, e2b);
-  const uint32_t e2 = (e1 & kEntryState) ? e2b : e2a;
-  const bool end1 = (e1 & kEntryEnd) != 0;
-  const uint32_t p1 = (e1 >> 10) & 15u;
-  // both combinations computed, then selected (no branch on end1)
-  const uint32_t ones2 = (e1 & kChunkMask) | ((e2 & kChunkMask) << p1);
-  const uint32_t npos2 = p1 + ((e2 >> 10) & 15u);
-  const uint32_t used2 = (uint32_t)kChunkBits + ((e2 >> 14) & 15u);
-  const uint32_t ones = end1 ? (e1 & kChunkMask) : ones2;
-  const uint32_t npos = end1 ? p1 : npos2;
-  const uint32_t used = end1 ? (e1 >> 14) & 15u : used2;
-  const bool ended = ((e1 | e2) & kEntryEnd) != 0;
+  // chunk 1 starts at the leading group test (table state 2), chunk 2 is read
+  // in both states and chosen by chunk 1's exit state; nothing follows a
+  // chunk 1 that ended the code
+  uint32_t e1, e2a, e2b;
+  rd.chunks(g, n < N, e1, e2a, e2b);
+  const uint32_t e2s = (e1 & kEntryState) ? e2b : e2a;
+  const uint32_t e2 = keep_if_bit13(e2s, e1);  // nothing after a chunk 1 that ended
+  const uint32_t S = e1 + e2;                  // field-wise sums
+  const uint32_t npos = S >> kPosShift & 31u;
+  const uint32_t used = S & kUsedMask;         // >= kNotEnded: the code has not ended
+  const uint32_t ones = ((e1 >> kOnesShift) & kChunkMask) |
+                        (((e2 >> kOnesShift) & kChunkMask) << ((e1 >> kPosShift) & 31u));
   // The stream reads as zeros past the block's last bit (the kernels and the
   // host reader guarantee it) and the budget always ends there, so a code
   // whose last one is the budget's last bit ends here one bit past the budget
   // (its zero group test is not in the stream): the reference keeps that one
   // and reads no more (decode.c:302-317).  Any other code the budget cuts
-  // short takes the general decoder.  (Decoding those here too costs the
-  // common case more than it saves.)
-  const bool ok = ended && used <= b1 + 1 && n + npos <= N - 1;
-  slow = gx && !ok;
-  const bool take = gx && ok;
-  const uint32_t ones_f = ones, npos_f = npos, used_f = umin(used, b1);
-  x |= (PW)(take ? ones_f : 0u) << (n & (8 * sizeof(PW) - 1));
-  n += take ? npos_f : 0u;
-  const unsigned adv = m + (take ? used_f : 0u);
+  // short takes the general decoder.  (N - 1 - n is huge for n = N.)
+  slow = !(used <= b1 + 1 && npos <= N - 1 - n);
+  // the verbatim bits below m, the new ones at n >= m: one v_bfi_b32 a dword
+  const PW o = (PW)ones << (n & (8 * sizeof(PW) - 1));
+  const PW x = ((PW)vmask & (PW)w) | (~(PW)vmask & o);
+  n += npos;
+  const unsigned adv = m + umin(used, b1);
   rd.pos += adv;
   bits -= adv;
   return x;
@@ -1017,8 +1072,8 @@ ZFP_HD void decode_half(planes<UInt, DIMS>& P, unsigned& bits, unsigned& n, int 
   typedef typename plane_word<DIMS>::type PW;
   int c = 31;
   for (; c - 1 >= cmin; c -= 2) {
-    if (!bits) return;
-    progress_priority(uniform(c));
+    if (!any_lane(bits != 0)) return;
+    progress_priority<CUZFP_DPRIO_T2, CUZFP_DPRIO_T1, CUZFP_DPRIO_T0>(uniform(c));
     const PW xa = decode_plane_any<DIMS, PW>(bits, n, rd);
     const PW xb = decode_plane_any<DIMS, PW>(bits, n, rd);
     const int u = uniform(c);
@@ -1106,7 +1161,8 @@ template <> struct fp<double> {
 // Writer: full() is true once the block's maxbits bits are written; while it is
 //   false, put(value, n) appends n <= 64 low bits (value has no bits at or
 //   above n; bits past maxbits are dropped) and zero_bit() appends one 0;
-//   finish() zero-pads the block to maxbits.
+//   finish() zero-pads the block to maxbits; settle() is called before each
+//   plane step and lets a full writer take (and discard) further steps.
 // Reader: peek() returns the next 64 stream bits, skip(n) consumes n <= 64.
 
 template <typename Scalar, int DIMS, typename Writer>
@@ -1268,6 +1324,9 @@ ZFP_HD void decode_block(Scalar* f, unsigned maxbits, Reader& rd) {
 #else
   planes<UInt, DIMS> P;
   decode_planes<UInt, DIMS>(P, budget, maxprec, rd);
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(CUZFP_NO_PRIO) && CUZFP_DPRIO_AFTER >= 0
+  __builtin_amdgcn_s_setprio(CUZFP_DPRIO_AFTER);  // see progress_priority
+#endif
   ZFP_STAMP(1);
   P.store(u);
   ZFP_STAMP(2);

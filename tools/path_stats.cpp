@@ -21,8 +21,13 @@ struct Rd {
   void init(size_t p) { pos = p; }
   void windows(unsigned m, uint64_t& w, uint32_t& g) { w = peek(); pos += m; g = (uint32_t)peek(); pos -= m; }
   static const cuzfp::ChunkLut& table() { static const cuzfp::ChunkLut t = cuzfp::make_chunk_lut(); return t; }
-  uint32_t lut(uint32_t i) const { return table().e[i]; }
-  void lut2(uint32_t i, uint32_t& a, uint32_t& b) const { a = table().e[i]; b = table().e[i + (1u << cuzfp::kChunkBits)]; }
+  void chunks(uint32_t g, bool group, uint32_t& e1, uint32_t& e2a, uint32_t& e2b) const {
+    const uint32_t* t = table().e;
+    const uint32_t c2 = (g >> cuzfp::kChunkBits) & cuzfp::kChunkMask;
+    e1 = t[group ? (2u << cuzfp::kChunkBits) | (g & cuzfp::kChunkMask) : cuzfp::kNoGroupEntry];
+    e2a = t[c2];
+    e2b = t[c2 + (1u << cuzfp::kChunkBits)];
+  }
 };
 struct Wr {
   uint64_t* s; size_t pos, end;
@@ -33,6 +38,7 @@ struct Wr {
     if (!n) return;
     unsigned sh = pos & 63; s[pos >> 6] |= v << sh; if (sh + n > 64) s[(pos >> 6) + 1] |= v >> (64 - sh); pos += n;
   }
+  void settle() {}
   void zero_bit() { if (pos < end) pos++; }
   void finish() {}
   uint32_t spread(uint32_t b) const { static const cuzfp::SpreadLut t = cuzfp::make_spread_lut(); return t.e[b]; }

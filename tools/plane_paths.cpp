@@ -17,6 +17,7 @@ struct Wr {
     if (!n) return;
     unsigned sh = pos & 63; s[pos >> 6] |= v << sh; if (sh + n > 64) s[(pos >> 6) + 1] |= v >> (64 - sh); pos += n;
   }
+  void settle() {}
   void zero_bit() { if (pos < end) pos++; }
   void finish() {}
   uint32_t spread(uint32_t b) const { static const cuzfp::SpreadLut t = cuzfp::make_spread_lut(); return t.e[b]; }

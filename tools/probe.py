@@ -92,7 +92,9 @@ for name, fn in (("encode", lambda: cz.encode(x, mb, out=w)), ("decode", lambda:
     for _ in range(3): fn()
     torch.cuda.synchronize()
     lib.cuzfp_hip_probe_clear()
-    fn(); torch.cuda.synchronize()
+    # back to back, as in the bench: the second launch's stamps overwrite the first's
+    for _ in range(@BACK@): fn()
+    torch.cuda.synchronize()
     buf = np.zeros(65536 * 10, np.uint64)
     lib.cuzfp_hip_probe_stamps(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes))
     np.save(os.path.join(@OUTDIR@, "stamps_" + name + "_" + @FIELD@ + "_" + str(@SIZE@) + ".npy"), buf.reshape(-1, 10)[:nw])
@@ -100,10 +102,10 @@ print("ok")
 """
 
 
-def stamps(size, field, outdir):
+def stamps(size, field, outdir, back=1):
     lib = os.path.join(OUT, "p9", "libcuzfp_hip.so")
     code = STAMP_CODE.replace("@ROOT@", repr(ROOT)).replace("@LIB@", repr(lib)).replace("@SIZE@", str(size)) \
-        .replace("@FIELD@", repr(field)).replace("@OUTDIR@", repr(outdir))
+        .replace("@FIELD@", repr(field)).replace("@OUTDIR@", repr(outdir)).replace("@BACK@", str(back))
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     if r.returncode:
         print(r.stderr[-3000:])
@@ -147,12 +149,13 @@ if __name__ == "__main__":
     ap.add_argument("cmd")
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--field", default="polynomial")
+    ap.add_argument("--back", type=int, default=1, help="stamped launches back to back (the last one's stamps)")
     a = ap.parse_args()
     if a.cmd == "build":
         build()
     elif a.cmd == "stamps":
         od = os.path.join(ROOT, "gpurun_out")
         os.makedirs(od, exist_ok=True)
-        stamps(a.size, a.field, od)
+        stamps(a.size, a.field, od, a.back)
     else:
         run(a.size, a.field)
