@@ -520,9 +520,16 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
     rd.lut32 = lut;
     rd.init(0);
     Scalar f[N];
-    decode_block<Scalar, DIMS>(f, g.maxbits, rd);
+    const bool coded = decode_block<Scalar, DIMS>(f, g.maxbits, rd);
     __builtin_amdgcn_s_setprio(3);  // a wave out of the coder stores at once
-    scatter<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
+    if (coded) {
+      scatter<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
+    } else {  // a zero block
+      Scalar z[N];
+#pragma unroll
+      for (int i = 0; i < N; i++) z[i] = (Scalar)0;
+      scatter<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), z);
+    }
   }
   ZFP_STAMP(6);
   ZFP_STAMP_REAL(9);

@@ -663,12 +663,12 @@ ZFP_HD uint64_t shl64(uint64_t v, uint32_t s) {
 #endif
 }
 
-template <int DIMS, typename PW, typename Writer>
+template <int DIMS, bool CHECK = true, typename PW, typename Writer>
 ZFP_HD bool encode_plane_lut(PW x, unsigned& n, Writer& wr) {
   constexpr unsigned N = 1u << (2 * DIMS);
   const uint64_t xx = (uint64_t)x;
   const uint64_t r = n < N ? xx >> (n & 63) : 0ull;
-  if (r >> 16) return false;
+  if (CHECK && (r >> 16)) return false;
   const uint64_t v = xx ^ shl64(r, n);  // the verbatim bits x & lowmask(n)
   const uint32_t rl = (uint32_t)r, b0 = rl & 0xffu, b1 = rl >> 8;
   const uint32_t p0 = (uint32_t)__builtin_popcount(b0);
@@ -691,7 +691,15 @@ ZFP_HD bool encode_plane_lut(PW x, unsigned& n, Writer& wr) {
 
 template <int DIMS, typename PW, typename Writer>
 ZFP_HD void encode_plane_any(PW x, unsigned& n, Writer& wr) {
-  if (__builtin_expect(!encode_plane_lut<DIMS>(x, n, wr), 0)) encode_plane<DIMS>(x, n, wr);
+  // one wave-uniform test: the per-lane branch around the table coder costs
+  // ~6 exec-mask instructions a plane even when no lane takes it
+  constexpr unsigned N = 1u << (2 * DIMS);
+  const uint64_t r = n < N ? (uint64_t)x >> (n & 63) : 0ull;
+  if (__builtin_expect(any_lane((r >> 16) != 0), 0)) {
+    if (!encode_plane_lut<DIMS>(x, n, wr)) encode_plane<DIMS>(x, n, wr);
+  } else {
+    encode_plane_lut<DIMS, false>(x, n, wr);
+  }
 }
 
 // Planes 31 .. cmin of 32-bit half H, two at a time (an odd one left at the
@@ -1057,22 +1065,26 @@ ZFP_HD PW decode_plane_any(unsigned& bits, unsigned& n, Reader& rd) {
   const unsigned n0 = n, bits0 = bits;
   bool slow;
   PW x = decode_plane_lut<DIMS, PW>(bits, n, rd, slow);
-  if (__builtin_expect(slow, 0)) {
-    rd.init(pos0);
-    n = n0;
-    bits = bits0;
-    x = decode_plane<DIMS, PW>(bits, n, rd);
+  if (__builtin_expect(any_lane(slow), 0)) {  // wave-uniform test first (see encode_plane_any)
+    if (slow) {
+      rd.init(pos0);
+      n = n0;
+      bits = bits0;
+      x = decode_plane<DIMS, PW>(bits, n, rd);
+    }
   }
   return x;
 }
 
-// Planes 31 .. cmin of 32-bit half H, two per loop trip.
+// Planes 31 .. cmin of 32-bit half H, two per loop trip, while any lane of the
+// wave has budget (a lane without deposits zeros).  Returns the highest plane
+// left unset (-1: none); those below it are unset too.
 template <int H, typename UInt, int DIMS, typename Reader>
-ZFP_HD void decode_half(planes<UInt, DIMS>& P, unsigned& bits, unsigned& n, int cmin, Reader& rd) {
+ZFP_HD int decode_half(planes<UInt, DIMS>& P, unsigned& bits, unsigned& n, int cmin, Reader& rd) {
   typedef typename plane_word<DIMS>::type PW;
   int c = 31;
   for (; c - 1 >= cmin; c -= 2) {
-    if (!any_lane(bits != 0)) return;
+    if (!any_lane(bits != 0)) return c;
     progress_priority<CUZFP_DPRIO_T2, CUZFP_DPRIO_T1, CUZFP_DPRIO_T0>(uniform(c));
     const PW xa = decode_plane_any<DIMS, PW>(bits, n, rd);
     const PW xb = decode_plane_any<DIMS, PW>(bits, n, rd);
@@ -1080,7 +1092,28 @@ ZFP_HD void decode_half(planes<UInt, DIMS>& P, unsigned& bits, unsigned& n, int 
     P.template set<H>(u, xa);
     P.template set<H>(u - 1, xb);
   }
-  if (c >= cmin && c >= 0 && bits) P.template set<H>(uniform(c), decode_plane_any<DIMS, PW>(bits, n, rd));
+  if (c >= cmin && c >= 0 && any_lane(bits != 0)) {
+    P.template set<H>(uniform(c), decode_plane_any<DIMS, PW>(bits, n, rd));
+    c--;
+  }
+  return c;
+}
+
+// Planes left unset by the loop must read as zero.  In 3D (set() assigns a
+// whole plane) only those are zeroed, after the loop; zeroing the whole array
+// before it costs ~90 moves a wave (the compiler then also shuffles the array
+// into the layout its indexed moves use).  1D/2D planes share registers and
+// set() ORs, so that array is zeroed up front.  (CUZFP_EAGER_ZERO: zero up
+// front in 3D too.)
+#ifndef CUZFP_EAGER_ZERO
+constexpr bool kLazyZero = true;
+#else
+constexpr bool kLazyZero = false;
+#endif
+template <int H, typename UInt, int DIMS>
+ZFP_HD void zero_planes(planes<UInt, DIMS>& P, int c) {
+  if constexpr (kLazyZero && DIMS == 3)
+    for (; c >= 0; c--) P.template set<H>(uniform(c), 0);
 }
 
 template <typename UInt, int DIMS, typename Reader>
@@ -1088,12 +1121,15 @@ ZFP_HD void decode_planes(planes<UInt, DIMS>& P, unsigned budget, unsigned maxpr
   constexpr int PREC = (int)sizeof(UInt) * 8;
   const int kmin = PREC > (int)maxprec ? PREC - (int)maxprec : 0;
   unsigned bits = budget, n = 0;
-  P.zero();
+  if constexpr (!(kLazyZero && DIMS == 3)) P.zero();
   if constexpr (PREC == 64) {
-    decode_half<1>(P, bits, n, kmin > 32 ? kmin - 32 : 0, rd);
-    if (kmin >= 32) return;
+    zero_planes<1>(P, decode_half<1>(P, bits, n, kmin > 32 ? kmin - 32 : 0, rd));
+    if (kmin >= 32) {
+      zero_planes<0>(P, 31);
+      return;
+    }
   }
-  decode_half<0>(P, bits, n, kmin, rd);
+  zero_planes<0>(P, decode_half<0>(P, bits, n, kmin, rd));
 }
 
 // ---------------------------------------------------------------------------
@@ -1199,10 +1235,17 @@ ZFP_HD void encode_block(const Scalar* f, unsigned maxbits, Writer& wr) {
     typedef float f2 __attribute__((ext_vector_type(2)));
     bool fast = false;
     if constexpr (sizeof(Scalar) == 4 && N % 2 == 0) {
-      f2 acc = {(float)f[0], (float)f[1]};
+      // four independent chains: one chain of dependent v_pk_add_f32 stalls a
+      // cycle (an s_nop) per add
+      constexpr int C = N >= 8 ? 4 : 1;
+      f2 acc[C];
 #pragma unroll
-      for (int i = 2; i < N; i += 2) acc += f2{(float)f[i], (float)f[i + 1]};
-      fast = emax >= -97 && __builtin_isfinite(acc.x + acc.y);
+      for (int c = 0; c < C; c++) acc[c] = f2{(float)f[2 * c], (float)f[2 * c + 1]};
+#pragma unroll
+      for (int i = 2 * C; i < N; i += 2) acc[(i / 2) % C] += f2{(float)f[i], (float)f[i + 1]};
+#pragma unroll
+      for (int c = 1; c < C; c++) acc[0] += acc[c];
+      fast = emax >= -97 && __builtin_isfinite(acc[0].x + acc[0].y);
     }
     if constexpr (sizeof(Scalar) == 4 && N % 2 == 0) {
       if (fast) {
@@ -1282,8 +1325,11 @@ ZFP_HD void encode_block(const Scalar* f, unsigned maxbits, Writer& wr) {
   wr.finish();
 }
 
+// Returns false, leaving f untouched, for a zero block (the caller stores
+// zeros: zeroing f here costs the kernel 64 register moves a wave, made on
+// every path before the branch).
 template <typename Scalar, int DIMS, typename Reader>
-ZFP_HD void decode_block(Scalar* f, unsigned maxbits, Reader& rd) {
+ZFP_HD bool decode_block(Scalar* f, unsigned maxbits, Reader& rd) {
   typedef traits<Scalar> T;
   typedef typename T::Int Int;
   typedef typename T::UInt UInt;
@@ -1293,11 +1339,7 @@ ZFP_HD void decode_block(Scalar* f, unsigned maxbits, Reader& rd) {
   if constexpr (!T::is_int) {
     // decode.c:352-381
     const uint64_t head = rd.peek();
-    if (!(head & 1)) {
-#pragma unroll
-      for (int i = 0; i < N; i++) f[i] = (Scalar)0;
-      return;
-    }
+    if (!(head & 1)) return false;
     emax = (int)((head >> 1) & lowmask(T::ebits)) - T::ebias;
     rd.skip(T::ebits + 1);
     maxprec = precision<DIMS>(emax, T::prec);
@@ -1359,6 +1401,7 @@ ZFP_HD void decode_block(Scalar* f, unsigned maxbits, Reader& rd) {
 #pragma unroll
     for (int i = 0; i < N; i++) f[i] = (Scalar)(Int)q[i];
   }
+  return true;
 }
 
 // ---------------------------------------------------------------------------

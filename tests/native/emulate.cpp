@@ -121,7 +121,8 @@ size_t run(bool enc, unsigned nx, unsigned ny, unsigned nz, long long sx, long l
       cuzfp::encode_block<Scalar, DIMS>(f, maxbits, wr);
     } else {
       HostReader rd{stream, words, b * (size_t)maxbits, (b + 1) * (size_t)maxbits};
-      cuzfp::decode_block<Scalar, DIMS>(f, maxbits, rd);
+      if (!cuzfp::decode_block<Scalar, DIMS>(f, maxbits, rd))
+        for (int i = 0; i < N; i++) f[i] = (Scalar)0;
       for (int i = 0; i < N; i++)
         if (valid[i]) data[off[i]] = f[i];
     }

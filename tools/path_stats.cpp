@@ -77,7 +77,8 @@ int main(int argc, char** argv) {
       g_calls = 0;
       Rd r{s.data(), b * maxbits};
       float f[64];
-      cuzfp::decode_block<float, 3>(f, maxbits, r);
+      if (!cuzfp::decode_block<float, 3>(f, maxbits, r))
+        for (int i = 0; i < 64; i++) f[i] = 0.0f;
       for (int c = 0; c < g_calls && c < 64; c++) { seen[c][g_path[c]] = 1; lane_cnt[g_path[c]]++; }
       if (g_calls > maxcalls) maxcalls = g_calls;
     }

@@ -61,6 +61,20 @@ int main() {
   hipEventCreate(&e1);
   BigArgs big{};
   big.w[40] = waves;
+  // back-to-back launches (as in the bench): per-launch time minus the spin is
+  // the launch + drain overhead a kernel pays in a stream of kernels
+  for (uint32_t spin_us : {0u, 20u}) {
+    for (int rep = 0; rep < 2; rep++) {
+      hipEventRecord(e0);
+      for (int k = 0; k < 50; k++)
+        hipLaunchKernelGGL(timeline, dim3(waves / 4), dim3(256), 33 * 1024, 0, t, spin_us * 100);
+      hipEventRecord(e1);
+      hipEventSynchronize(e1);
+      float ms = 0;
+      hipEventElapsedTime(&ms, e0, e1);
+      if (rep) printf("back-to-back, spin %2u us: %.2f us per launch\n", spin_us, ms * 1000 / 50);
+    }
+  }
   for (int variant = 0; variant < 2; variant++)
   for (uint32_t spin_us : {0u, 5u, 20u}) {
     const uint32_t ticks = spin_us * 100;
