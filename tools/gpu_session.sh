@@ -72,11 +72,11 @@ for s in $STEPS; do
       done ;;
     stamps)
       # per-wave phase timestamps (s_memtime) of the diagnostic build
-      timeout -k 10 300 python tools/probe.py stamps > "$OUT/stamps_$TAG.log" 2>&1
+      timeout -k 10 300 python tools/probe.py stamps --back 4 > "$OUT/stamps_$TAG.log" 2>&1
       ok_or_stop $? stamps
-      timeout -k 10 300 python tools/probe.py stamps --field splitmix >> "$OUT/stamps_$TAG.log" 2>&1
+      timeout -k 10 300 python tools/probe.py stamps --back 4 --field splitmix >> "$OUT/stamps_$TAG.log" 2>&1
       ok_or_stop $? stamps_split
-      timeout -k 10 300 python tools/probe.py stamps --size 512 >> "$OUT/stamps_$TAG.log" 2>&1
+      timeout -k 10 300 python tools/probe.py stamps --back 4 --size 512 >> "$OUT/stamps_$TAG.log" 2>&1
       ok_or_stop $? stamps_512; cat "$OUT/stamps_$TAG.log" ;;
     probe)
       # phase costs: product kernels vs no plane coder vs no transpose (tools/probe.py)
