@@ -380,12 +380,6 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
   // lds[64 j + l] (conflict-free ds_or_b64 whatever each lane's bit position),
   // W words per block plus kSlackWords rows
   const uint32_t W = g.maxbits >> 6;
-#ifdef CUZFP_STAGGER
-  {  // experiment: the k-th quarter of the grid (a SIMD's k-th wave) loads k steps later
-    const uint32_t rank = blockIdx.x * 4 / gridDim.x;
-    for (uint32_t r = 0; r < rank; r++) __builtin_amdgcn_s_sleep(CUZFP_STAGGER);
-  }
-#endif
   Scalar f[N];
   if (b < g.nblocks) gather<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
   ((uint4*)lut)[lane] = spread16;  // every lane: the table is the wave's

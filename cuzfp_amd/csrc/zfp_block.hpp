@@ -136,9 +136,12 @@ template <int... I> struct seq_gen<0, I...> { typedef seq<I...> type; };
 template <int N> using make_seq = typename seq_gen<N>::type;
 template <int DIMS, int I> struct pidx { static constexpr int value = perm<DIMS>::at(I); };
 
+// (q + nb) ^ nb in coefficient order, without the final "^ nb": the encoder
+// applies that after the bit-plane transpose, where it inverts the odd planes
+// for free (planes::load<true>)
 template <int DIMS, typename UInt, int... I>
-ZFP_HD void permute_fwd(const UInt* q, UInt* u, UInt nb, seq<I...>) {
-  ((u[I] = (q[pidx<DIMS, I>::value] + nb) ^ nb), ...);
+ZFP_HD void permute_fwd_add(const UInt* q, UInt* u, UInt nb, seq<I...>) {
+  ((u[I] = q[pidx<DIMS, I>::value] + nb), ...);
 }
 // (u ^ nb) - nb: one v_xad_u32 ((a ^ b) + c) for 32-bit words on the device
 ZFP_HD uint32_t from_negabinary(uint32_t u, uint32_t nb) {
@@ -262,6 +265,17 @@ ZFP_HD uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {
 #endif
 }
 
+// ~((a & m) | (b & ~m)) in one v_bitop3_b32 (truth table 0x35: not of v_bfi's 0xca)
+ZFP_HD uint32_t nbfi(uint32_t m, uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x35" : "=v"(r) : "s"(m), "v"(a), "v"(b));
+  return r;
+#else
+  return ~((a & m) | (b & ~m));
+#endif
+}
+
 // bytes of {a = bytes 0-3, b = bytes 4-7} picked by sel (v_perm_b32)
 ZFP_HD uint32_t perm_bytes(uint32_t b, uint32_t a, uint32_t sel) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -274,7 +288,8 @@ ZFP_HD uint32_t perm_bytes(uint32_t b, uint32_t a, uint32_t sel) {
 #endif
 }
 
-template <int J>
+// INV (last stage only): the odd output words come out inverted
+template <int J, bool INV = false>
 ZFP_HD void transpose_stage(uint32_t* a, int rows) {
   // swap the J x J off-diagonal sub-blocks of every 2J x 2J tile:
   //   lo' = (lo & m) | ((hi << J) & ~m),  hi' = ((lo >> J) & m) | (hi & ~m)
@@ -293,19 +308,21 @@ ZFP_HD void transpose_stage(uint32_t* a, int rows) {
       a[i + J] = perm_bytes(hi, lo, 0x07030501u);
     } else {
       a[i] = bfi(m, lo, hi << J);
-      a[i + J] = bfi(m, lo >> J, hi);
+      a[i + J] = INV ? nbfi(m, lo >> J, hi) : bfi(m, lo >> J, hi);
     }
   }
 }
 
-template <int R>
+// NEG_ODD: invert the odd output words, i.e. (R even) the odd planes -- the
+// "^ 0xaaaa..." of the negabinary conversion, applied to planes
+template <int R, bool NEG_ODD = false>
 ZFP_HD void transpose_tiles(uint32_t* a) {
   // stages J = R/2, ..., 1 spelled out so every index is a compile-time constant
   if constexpr (R >= 32) transpose_stage<16>(a, R);
   if constexpr (R >= 16) transpose_stage<8>(a, R);
   if constexpr (R >= 8) transpose_stage<4>(a, R);
   if constexpr (R >= 4) transpose_stage<2>(a, R);
-  if constexpr (R >= 2) transpose_stage<1>(a, R);
+  if constexpr (R >= 2) transpose_stage<1, NEG_ODD>(a, R);
 }
 
 // Planes of N = 4^DIMS coefficients held as 32-bit words.  For 32-bit
@@ -327,6 +344,9 @@ template <typename UInt, int DIMS> struct planes {
   typedef uint32_t vec __attribute__((ext_vector_type(R)));
   vec v[H][G];
 
+  // NEG_ODD: u holds q + 0xaaaa... and the planes get the negabinary's
+  // final "^ 0xaaaa..." (the odd planes inverted) from the transpose
+  template <bool NEG_ODD = false>
   ZFP_HD void load(const UInt* u) {
     uint32_t w[H][N];
 #pragma unroll
@@ -337,7 +357,7 @@ template <typename UInt, int DIMS> struct planes {
 #pragma unroll
     for (int h = 0; h < H; h++)
 #pragma unroll
-      for (int g = 0; g < G; g++) transpose_tiles<R>(&w[h][g * R]);
+      for (int g = 0; g < G; g++) transpose_tiles<R, NEG_ODD>(&w[h][g * R]);
 #pragma unroll
     for (int h = 0; h < H; h++)
 #pragma unroll
@@ -551,62 +571,6 @@ ZFP_HD void progress_priority(int c) {
 #else
   (void)c;
 #endif
-}
-
-// Group code of the not-yet-significant part r of a plane (see encode_plane):
-// G and its length L; dense is set (and G, L are not) when G would not fit 64
-// bits.
-template <int DIMS, typename PW>
-struct group_code {
-  uint64_t G;
-  unsigned L, adv;  // adv: how far n moves
-  bool dense;
-};
-
-// Two consecutive planes per step: both planes' codes are built before any is
-// written (plane B only needs n after plane A, one add), and their new ones
-// are spread by one merged loop, so the step has two independent chains and
-// half the loop overhead of plane-at-a-time coding.  Writers drop bits past
-// maxbits (the word writer into its slack), so plane B is written even when
-// plane A filled the block.
-template <int DIMS, typename PW, typename Writer>
-ZFP_HD void encode_plane_pair(PW xa, PW xb, unsigned& n, Writer& wr) {
-  constexpr unsigned N = 1u << (2 * DIMS);
-  constexpr unsigned SH = 8 * sizeof(PW) - 1;
-  const PW ra = n < N ? (PW)(xa >> (n & SH)) : (PW)0;
-  const unsigned ta = (unsigned)(sizeof(PW) == 8 ? __builtin_popcountll((uint64_t)ra) : __builtin_popcount((uint32_t)ra));
-  const unsigned pa = ra ? (unsigned)(8 * sizeof(PW) - 1) - (unsigned)(sizeof(PW) == 8 ? __builtin_clzll((uint64_t)ra) : __builtin_clz((uint32_t)ra)) : 0u;
-  const unsigned na = n + (ra ? pa + 1 : 0u);
-  const PW rb = na < N ? (PW)(xb >> (na & SH)) : (PW)0;
-  const unsigned tb = (unsigned)(sizeof(PW) == 8 ? __builtin_popcountll((uint64_t)rb) : __builtin_popcount((uint32_t)rb));
-  const unsigned pb = rb ? (unsigned)(8 * sizeof(PW) - 1) - (unsigned)(sizeof(PW) == 8 ? __builtin_clzll((uint64_t)rb) : __builtin_clz((uint32_t)rb)) : 0u;
-  const unsigned qa = pa + ta - 1, qb = pb + tb - 1;
-  if (__builtin_expect((ra && qa > 61) || (rb && qb > 61), 0)) {  // a dense plane
-    encode_plane<DIMS>(xa, n, wr);
-    encode_plane<DIMS>(xb, n, wr);
-    return;
-  }
-  uint64_t Fa = 0, Fb = 0;
-  PW a = ra, b = rb;
-  unsigned j = 0;
-  while (a | b) {  // F |= (j-th one) << j, both planes at once
-    const PW la = a & (PW)(0 - a), lb = b & (PW)(0 - b);
-    Fa |= (uint64_t)la << j;
-    Fb |= (uint64_t)lb << j;
-    a ^= la;
-    b ^= lb;
-    j++;
-  }
-  const bool lasta = pa + n == N - 1, lastb = pb + na == N - 1;
-  const unsigned La = ra ? qa + (lasta ? 1u : 3u) : (n < N ? 1u : 0u);
-  const unsigned Lb = rb ? qb + (lastb ? 1u : 3u) : (na < N ? 1u : 0u);
-  const uint64_t Ga = ra ? (1ull | (Fa << 1) | (Fa << 2)) & lowmask(lasta ? La : La - 1) : 0ull;
-  const uint64_t Gb = rb ? (1ull | (Fb << 1) | (Fb << 2)) & lowmask(lastb ? Lb : Lb - 1) : 0ull;
-  wr.put(xa & (PW)lowmask(n), n);
-  wr.put(Ga, La);
-  wr.put(xb & (PW)lowmask(na), na);
-  wr.put(Gb, Lb);
-  n = na + (rb ? pb + 1 : 0u);
 }
 
 // Table-driven plane step (the common case).  The group code of the plane's
@@ -1298,7 +1262,7 @@ ZFP_HD void encode_block(const Scalar* f, unsigned maxbits, Writer& wr) {
   fwd_xform<DIMS>(q);
   UInt u[N];
   constexpr UInt NB = nbmask<UInt>::value;
-  permute_fwd<DIMS>(q, u, NB, make_seq<N>());
+  permute_fwd_add<DIMS>(q, u, NB, make_seq<N>());  // "^ NB" in P.load<true>
   ZFP_STAMP(2);
 #if defined(CUZFP_PROBE) && (CUZFP_PROBE == 1 || CUZFP_PROBE == 2)
   // timing probes (tools/probe.py; never built into the product library):
@@ -1317,7 +1281,7 @@ ZFP_HD void encode_block(const Scalar* f, unsigned maxbits, Writer& wr) {
   (void)maxprec;
 #else
   planes<UInt, DIMS> P;
-  P.load(u);
+  P.template load<true>(u);
   ZFP_STAMP(3);
   encode_planes<UInt, DIMS>(P, maxprec, wr);
   ZFP_STAMP(4);
