@@ -287,3 +287,24 @@ def test_random_streams(cuda, restatement, dims, dtype):
                np.dtype(np.int32): torch.int32, np.dtype(np.int64): torch.int64}[np.dtype(dtype)]
         got = cz.decode(d, shape, tdt, mb).cpu().numpy()
         assert np.array_equal(got.view(np.uint8), want.view(np.uint8)), (shape, mb, density)
+
+
+# --------------------------------------------------------------------------
+# persistent 1D/2D launches: more batches than resident waves (each wave codes
+# several), a partial last batch, strided / padded fields on the same path
+
+
+@pytest.mark.parametrize("dims,shape", [(1, (3 * 2 ** 20 + 7,)), (2, (2050, 1030)), (1, (5 * 2 ** 20,))])
+@pytest.mark.parametrize("dtype", [np.float32, np.float64, np.int32])
+def test_persistent_batches(cuda, restatement, dims, shape, dtype):
+    rng = np.random.default_rng(hash((dims, shape, np.dtype(dtype).str)) % 2 ** 32)
+    if np.dtype(dtype).kind == "i":
+        a = rng.integers(-2 ** 24, 2 ** 24, size=shape).astype(dtype)
+    else:
+        a = _fields(rng, shape, dtype, "smooth")
+    for rate in (3, 8, 21):
+        mb = cz.rate_to_maxbits(rate, dtype, dims)
+        words, y = _gpu_roundtrip(a, mb, cuda)
+        ref = restatement.compress(a, mb)
+        assert np.array_equal(words, ref), rate
+        assert np.array_equal(y, restatement.decompress(ref, shape, dtype, mb)), rate
