@@ -189,6 +189,13 @@ struct LdsReader {
     e2a = ((lds_u32*)(uintptr_t)a2)[0];
     e2b = ((lds_u32*)(uintptr_t)a2)[1u << kChunkBits];
   }
+  __device__ __forceinline__ uint32_t chunk1(uint32_t g, bool group) const {
+    const uint32_t base = (uint32_t)(uintptr_t)(lds_u32*)lut32;
+    const uint32_t c1 = group ? (g & kChunkMask) : kNoGroupEntry - (2u << kChunkBits);
+    uint32_t a1;
+    asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a1) : "v"(c1), "s"(base));
+    return ((lds_u32*)(uintptr_t)a1)[2u << kChunkBits];
+  }
   __device__ __forceinline__ void load() {
     const uint32_t* r = lds32 + (pos >> 5) * 64;
     x0 = r[0];
@@ -462,7 +469,9 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
       if (4 * q < D) held[q] = src[q];
   }
   uint32_t* lut = (uint32_t*)(lds_all + (size_t)(blockDim.x >> 6) * g.lds_words);
-  for (uint32_t i = threadIdx.x; i < sizeof(ChunkLut) / 16; i += blockDim.x)
+  // (1D reads chunk-1 entries only: state 2 and the no-group entry)
+  constexpr uint32_t kLutFrom = DIMS == 1 ? (2u << kChunkBits) / 4 : 0;
+  for (uint32_t i = kLutFrom + threadIdx.x; i < sizeof(ChunkLut) / 16; i += blockDim.x)
     ((uint4*)lut)[i] = ((const uint4*)g_chunk_lut.e)[i];
   if (live) {
     if (vec) {

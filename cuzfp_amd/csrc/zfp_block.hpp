@@ -975,7 +975,8 @@ ZFP_HD uint32_t keep_if_bit13(uint32_t v, uint32_t e) {
 // One plane by table lookup.  Reader: windows(m, w, g) gives the 64 stream
 // bits at the read position (w) and the 32 bits m further on (g);
 // chunks(g, group, e1, e2a, e2b) reads the entry of g's first chunk in state 2
-// (the no-group entry when !group) and of its second chunk in states 0 and 1.
+// (the no-group entry when !group) and of its second chunk in states 0 and 1;
+// chunk1(g, group) only the first.
 // Sets `slow` for a plane the tables cannot finish (a code longer than two
 // chunks, one that runs into the budget, or one that reaches position N-1,
 // where the one is implied); the caller then discards this step's result and
@@ -995,10 +996,17 @@ ZFP_HD PW decode_plane_lut(unsigned& bits, unsigned& n, Reader& rd, bool& slow) 
   // chunk 1 starts at the leading group test (table state 2), chunk 2 is read
   // in both states and chosen by chunk 1's exit state; nothing follows a
   // chunk 1 that ended the code
-  uint32_t e1, e2a, e2b;
-  rd.chunks(g, n < N, e1, e2a, e2b);
-  const uint32_t e2s = (e1 & kEntryState) ? e2b : e2a;
-  const uint32_t e2 = keep_if_bit13(e2s, e1);  // nothing after a chunk 1 that ended
+  uint32_t e1, e2;
+  if constexpr (DIMS == 1) {
+    // a 1D code (4 positions, at most 7 bits with the leading test) fits chunk 1
+    e1 = rd.chunk1(g, n < N);
+    e2 = 0;
+  } else {
+    uint32_t e2a, e2b;
+    rd.chunks(g, n < N, e1, e2a, e2b);
+    const uint32_t e2s = (e1 & kEntryState) ? e2b : e2a;
+    e2 = keep_if_bit13(e2s, e1);  // nothing after a chunk 1 that ended
+  }
   const uint32_t S = e1 + e2;                  // field-wise sums
   const uint32_t npos = S >> kPosShift & 31u;
   const uint32_t used = S & kUsedMask;         // >= kNotEnded: the code has not ended

@@ -85,6 +85,9 @@ struct HostReader {
     e2a = t[c2];
     e2b = t[c2 + (1u << cuzfp::kChunkBits)];
   }
+  uint32_t chunk1(uint32_t g, bool group) const {
+    return table().e[group ? (2u << cuzfp::kChunkBits) | (g & cuzfp::kChunkMask) : cuzfp::kNoGroupEntry];
+  }
 };
 
 template <typename Scalar, int DIMS>

@@ -28,6 +28,9 @@ struct Rd {
     e2a = t[c2];
     e2b = t[c2 + (1u << cuzfp::kChunkBits)];
   }
+  uint32_t chunk1(uint32_t g, bool group) const {
+    return table().e[group ? (2u << cuzfp::kChunkBits) | (g & cuzfp::kChunkMask) : cuzfp::kNoGroupEntry];
+  }
 };
 struct Wr {
   uint64_t* s; size_t pos, end;
