@@ -636,8 +636,9 @@ ZFP_HD bool encode_plane_lut(PW x, unsigned& n, Writer& wr) {
   const uint64_t v = xx ^ shl64(r, n);  // the verbatim bits x & lowmask(n)
   const uint32_t rl = (uint32_t)r, b0 = rl & 0xffu, b1 = rl >> 8;
   const uint32_t p0 = (uint32_t)__builtin_popcount(b0);
-  const uint32_t t = p0 + (uint32_t)__builtin_popcount(b1);
-  const uint32_t E = wr.spread(b0) | (wr.spread(b1) << (8 + p0));   // r, ones doubled
+  // r, ones doubled (1D: r has at most 4 bits, one table read)
+  const uint32_t t = N <= 8 ? p0 : p0 + (uint32_t)__builtin_popcount(b1);
+  const uint32_t E = N <= 8 ? wr.spread(b0) : wr.spread(b0) | (wr.spread(b1) << (8 + p0));
   const uint32_t nz = rl ? 1u : 0u;                                   // any new ones
   const uint32_t bl = bitlen16(rl);                                   // positions covered
   const uint32_t L = bl + t;                                          // bits of E
@@ -658,6 +659,10 @@ ZFP_HD void encode_plane_any(PW x, unsigned& n, Writer& wr) {
   // one wave-uniform test: the per-lane branch around the table coder costs
   // ~6 exec-mask instructions a plane even when no lane takes it
   constexpr unsigned N = 1u << (2 * DIMS);
+  if constexpr (N <= 16) {  // r has at most 16 bits: never dense
+    encode_plane_lut<DIMS, false>(x, n, wr);
+    return;
+  }
   const uint64_t r = n < N ? (uint64_t)x >> (n & 63) : 0ull;
   if (__builtin_expect(any_lane((r >> 16) != 0), 0)) {
     if (!encode_plane_lut<DIMS>(x, n, wr)) encode_plane<DIMS>(x, n, wr);
