@@ -46,9 +46,9 @@ os.environ['CUZFP_HIP_LIB'] = {lib!r}
 import cuzfp_amd as cz
 from cuzfp_amd.datagen import polynomial_field, splitmix_uniform
 shape = ({size},)*3
-arr = polynomial_field(shape) if {field!r} == 'polynomial' else splitmix_uniform(shape)
+arr = polynomial_field(shape, {dtype!r}) if {field!r} == 'polynomial' else splitmix_uniform(shape, {dtype!r})
 x = torch.from_numpy(arr).cuda()
-mb = cz.rate_to_maxbits(8, arr.dtype, 3)
+mb = cz.rate_to_maxbits({rate}, arr.dtype, 3)
 w = cz.encode(x, mb); y = cz.decode(w, shape, x.dtype, mb)
 def t(fn):
     for _ in range(5): fn()
@@ -57,14 +57,16 @@ def t(fn):
     for _ in range(40): fn()
     e1.record(); torch.cuda.synchronize()
     return round(e0.elapsed_time(e1) / 40 * 1000, 2)
-print(json.dumps(dict(enc_us=t(lambda: cz.encode(x, mb, out=w)), dec_us=t(lambda: cz.decode(w, shape, x.dtype, mb, out=y)))))
+def step():
+    cz.encode(x, mb, out=w); cz.decode(w, shape, x.dtype, mb, out=y)
+print(json.dumps(dict(enc_us=t(lambda: cz.encode(x, mb, out=w)), dec_us=t(lambda: cz.decode(w, shape, x.dtype, mb, out=y)), step_us=t(step))))
 """
 
 
-def run(names, size, field):
+def run(names, size, field, dtype="float32", rate=8):
     for name in names:
         lib = os.path.join(OUT, name, "libcuzfp_hip.so")
-        code = CODE.format(root=ROOT, lib=lib, size=size, field=field)
+        code = CODE.format(root=ROOT, lib=lib, size=size, field=field, dtype=dtype, rate=rate)
         r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
         if r.returncode:
             print(name, "FAILED", r.stderr[-500:])
@@ -82,6 +84,8 @@ if __name__ == "__main__":
         p.add_argument("cmd")
         p.add_argument("--size", type=int, default=256)
         p.add_argument("--field", default="polynomial")
+        p.add_argument("--dtype", default="float32")
+        p.add_argument("--rate", type=int, default=8)
         p.add_argument("names", nargs="+")
         a = p.parse_args()
-        run(a.names, a.size, a.field)
+        run(a.names, a.size, a.field, a.dtype, a.rate)
