@@ -232,20 +232,29 @@ struct LdsReader {
 // 16-byte access and consecutive lanes (consecutive x-blocks) read consecutive
 // 16-byte segments: 1 KiB per wave instruction.
 
-// The f32 decoder's value stores are non-temporal (global_store ... nt): its
-// output is written once, each store instruction covering 1 KiB of a row, and
-// keeping it out of the L2 takes the 256^3 decode from 33.4 to 29.9 us
-// (tools/variants.py; the encode+decode step gains ~1 %).  f64 rows are two
-// 16-byte stores a lane, each instruction covering every other 16 bytes, and
-// there the hint cost 32 % (61.5 -> 81.1 us), so f64 stores stay plain, as do
-// the encoder's gathers and the compressed stream (neutral or worse).
+// f32 values move with non-temporal hints (global_load/store ... nt): each
+// array is read or written once per kernel, each instruction covering 1 KiB
+// of a row.  At 256^3 the stores take the decode from 33.4 to 29.9 us and the
+// encode+decode step by 1.3 %; the gathers another 1-2 % of the step
+// (tools/variants.py).  f64 rows are two 16-byte accesses a lane, each
+// instruction covering every other 16 bytes, and there the store hint cost
+// 32 % (61.5 -> 81.1 us), so f64 stays plain, as does the compressed stream
+// (a hint on it measured neutral or worse).
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-#ifndef CUZFP_TEMPORAL_STORE
-constexpr bool kNtStore = true;
+#ifndef CUZFP_TEMPORAL_VALUES
+constexpr bool kNtValues = true;
 #else
-constexpr bool kNtStore = false;  // A/B builds
+constexpr bool kNtValues = false;  // A/B builds
 #endif
-__device__ __forceinline__ uint4 ld16(const void* p) { return *(const uint4*)p; }
+template <bool NT>
+__device__ __forceinline__ uint4 ld16(const void* p) {
+  if constexpr (NT) {
+    const u32x4 v = __builtin_nontemporal_load((const u32x4*)p);
+    return uint4{v.x, v.y, v.z, v.w};
+  } else {
+    return *(const uint4*)p;
+  }
+}
 template <bool NT>
 __device__ __forceinline__ void st16(void* p, uint4 v) {
   if constexpr (NT)
@@ -257,11 +266,11 @@ __device__ __forceinline__ void st16(void* p, uint4 v) {
 template <typename Scalar>
 __device__ __forceinline__ void load_row(const Scalar* p, Scalar* f) {
   if constexpr (sizeof(Scalar) == 4) {
-    const uint4 v = ld16(p);
+    const uint4 v = ld16<kNtValues>(p);
     __builtin_memcpy(f, &v, 16);
   } else {
-    const uint4 a = ld16(p);
-    const uint4 b = ld16(p + 2);
+    const uint4 a = ld16<false>(p);
+    const uint4 b = ld16<false>(p + 2);
     __builtin_memcpy(f, &a, 16);
     __builtin_memcpy(f + 2, &b, 16);
   }
@@ -272,7 +281,7 @@ __device__ __forceinline__ void store_row(Scalar* p, const Scalar* f) {
   if constexpr (sizeof(Scalar) == 4) {
     uint4 v;
     __builtin_memcpy(&v, f, 16);
-    st16<kNtStore>(p, v);
+    st16<kNtValues>(p, v);
   } else {
     uint4 a, b;
     __builtin_memcpy(&a, f, 16);
