@@ -47,6 +47,10 @@ def parse():
     p.add_argument("--dims", type=int, default=3, choices=[1, 2, 3],
                    help="1D / 2D arrays of edge --size (BASELINE configs 2D 8192^2 r2, 1D 1M r8); "
                         "the headline workload is 3D")
+    p.add_argument("--global-edge", type=int, default=0,
+                   help="3D only: shard one E^3 global array over the ranks as z-slabs of E/N planes "
+                        "(strong scaling; BASELINE configs[4] is E=1024 over 8 GPUs) instead of a "
+                        "--size^3 slab per rank")
     p.add_argument("--rate", type=float, default=8.0)
     p.add_argument("--dtype", default="float32", choices=["float32", "float64"])
     p.add_argument("--field", default="polynomial", choices=["polynomial", "splitmix"])
@@ -112,11 +116,19 @@ def main():
     dims = args.dims
     shape = (n,) * dims                                # this rank's slab
     gshape = (n * world,) + (n,) * (dims - 1)          # the global array
+    strong = args.global_edge > 0
+    if strong:
+        E = args.global_edge
+        if dims != 3 or E % (4 * world):
+            raise SystemExit(f"--global-edge needs 3D and an edge divisible by 4*N (got {E}, N={world})")
+        n = E
+        shape = (E // world, E, E)
+        gshape = (E, E, E)
     maxbits = cz.rate_to_maxbits(args.rate, dtype, dims)
     # each rank's slab: planes [rank*n, (rank+1)*n) of the global field
     if args.field == "polynomial":
         if dims == 3:
-            a = polynomial_slab(gshape, rank * n, (rank + 1) * n, dtype)
+            a = polynomial_slab(gshape, rank * shape[0], (rank + 1) * shape[0], dtype)
         else:
             from cuzfp_amd.datagen import polynomial_field
             a = polynomial_field(shape, dtype)
@@ -157,7 +169,7 @@ def main():
     gpath = os.path.join(ROOT, "tests", "golden", "golden.json")
     key = {("float32", 8.0): "baseline/3d_f32_256_r8", ("float64", 16.0): "baseline/3d_f64_256_r16"}.get(
         (args.dtype, args.rate))
-    if key and dims == 3 and n == 256 and world == 1 and os.path.exists(gpath):
+    if key and dims == 3 and n == 256 and world == 1 and not strong and os.path.exists(gpath):
         rec = json.load(open(gpath))["cases"].get(f"{key}/{args.field}")
         if rec:
             got = hashlib.sha256(words.cpu().numpy().tobytes()).hexdigest()
@@ -236,11 +248,12 @@ def main():
     dom_ms = max(enc_ms, dec_ms)
     dom_bytes = enc_bytes if dominant == "encode" else dec_bytes
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+    workload = f"{dims}d_{args.dtype}_{n}^{dims}_rate{args.rate:g}" + (f"_zslab{world}" if strong and world > 1 else "")
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            wk = f"{dims}d_{args.dtype}_{n}^{dims}_rate{args.rate:g}"
+            wk = workload
             if tj.get("workload") == wk:
                 traffic = tj.get(dominant + "_hbm_bytes_per_launch")
         except Exception:
@@ -249,7 +262,7 @@ def main():
     result = None
     if rank == 0:
         host_path = None
-        if world == 1 and not args.no_host_path:
+        if world == 1 and not args.no_host_path and not strong:
             hp_in = torch.from_numpy(a).pin_memory().numpy()
             hp_out = torch.empty(s_bytes // 8, dtype=torch.int64).pin_memory().numpy().view(np.uint64)
             hp_back = torch.empty(a.shape, dtype=x.dtype).pin_memory().numpy()
@@ -266,7 +279,7 @@ def main():
             host_path = {"compress_GBps": round(n_in / tc / 1e9, 2), "decompress_GBps": round(n_in / td / 1e9, 2),
                          "roundtrip_GBps": round(n_in / (tc + td) / 1e9, 2),
                          "note": "pinned host buffers, PCIe-inclusive (cuzfp_hip_compress_host/decompress_host)"}
-        cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(a, maxbits)
+        cpu = None if (args.no_cpu_baseline or world > 1 or strong) else cpu_baseline(a, maxbits)
         result = {
             "metric": METRIC if (dims == 3 and args.dtype == "float32") else
                       METRIC_OTHER.format(dims=dims, dt="f32" if args.dtype == "float32" else "f64"),
@@ -277,11 +290,11 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f32" if args.dtype == "float32" else "f64",
             "data": f"synthetic ({'testzfp polynomial field' if args.field == 'polynomial' else 'splitmix64 uniform [-1,1)'})",
-            "config": {"workload": f"{dims}d_{args.dtype}_{n}^{dims}_rate{args.rate:g}", "shape_per_gpu": list(shape),
+            "config": {"workload": workload, "shape_per_gpu": list(shape),
                        "global_shape": list(gshape), "maxbits": maxbits, "rate": args.rate,
                        "parallelism": f"z-slab x{world}", "stream_bytes_per_gpu": s_bytes},
             "pct_hbm_peak": round(100.0 * value / world * (enc_bytes + dec_bytes) / n_in / HBM_PEAK_GBS, 2),
