@@ -20,6 +20,7 @@
 // Instantiated per scalar type in inst_{f32,f64,i32,i64}.hip (parallel build).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #if defined(CUZFP_PROBE) && CUZFP_PROBE == 9
 // Diagnostic build (tools/probe.py stamps): lane 0 of every wave records
@@ -76,7 +77,9 @@ constexpr size_t kSpreadLutBytes = sizeof(SpreadLut);
 // pair of planes it is in: at most 2 x 128 bits + one straddled word) lands in
 // the slack, which the copy-out skips.
 constexpr uint32_t kSlackWords = 6;
+template <bool PRIO = true>
 struct LdsOrWriter {
+  static constexpr bool kPrio = PRIO;  // progress_priority schedule (zfp_block.hpp)
   uint64_t* p;          // the lane's column: word j at p[64 j], W + kSlackWords words, zeroed
   const uint32_t* lut;  // the workgroup's spread table
   uint32_t pos, lim;    // bits produced; 64 * W
@@ -99,7 +102,9 @@ struct LdsOrWriter {
 // general maxbits: the lane's bits are [pos0, end) of the wave's segment;
 // 64-bit chunks are OR-ed into the (zeroed) LDS image with ds_or_b64, since
 // the first and last words of a lane's range are shared with its neighbours.
+template <bool PRIO = true>
 struct LdsBitWriter {
+  static constexpr bool kPrio = PRIO;
   uint64_t* lds;
   const uint32_t* lut;     // the workgroup's spread table
   uint32_t pos, end, cnt;  // pos: stream offset of acc's bit 0
@@ -148,7 +153,9 @@ struct LdsBitWriter {
 // LDS reads for the new position at once.  The plane decoder skips as soon as
 // it knows where the next plane starts -- before it places the plane's ones --
 // so those reads land while it still has work to do.
+template <bool PRIO = true>
 struct LdsReader {
+  static constexpr bool kPrio = PRIO;
   const uint32_t* lds32;
   const uint32_t* lut32;  // the workgroup's copy of the chunk tables
   uint32_t pos;
@@ -389,7 +396,7 @@ template <typename Scalar, int DIMS> struct occupancy {
   static constexpr int value = (sizeof(Scalar) == 8 && DIMS == 3) ? 2 : 4;
 };
 
-template <typename Scalar, int DIMS, bool FAST, bool ALIGNED>
+template <typename Scalar, int DIMS, bool FAST, bool ALIGNED, bool PRIO = true>
 __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::value)) void zfp_encode(const Scalar* __restrict__ data,
                                                                       Geometry g,
                                                                       uint64_t* __restrict__ stream) {
@@ -405,7 +412,7 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
   // stream images): its load is issued first so that storing it waits only
   // for it, not for the block's gathers
   const uint4 spread16 = ((const uint4*)g_spread_lut.e)[lane];
-  __builtin_amdgcn_s_setprio(3);  // lowered through the plane loop (progress_priority)
+  if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);  // lowered through the plane loop (progress_priority)
   uint32_t* lut = (uint32_t*)(lds_all + (size_t)(blockDim.x >> 6) * g.lds_words) + wig * 256;
   ZFP_STAMP_HWID();
   ZFP_STAMP_REAL(8);
@@ -426,15 +433,15 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
       uint64_t* mine = lds + lane;
       for (uint32_t j = 0; j < W + kSlackWords; j++) mine[j * 64] = 0;  // own column
       wave_lds_sync();  // the wave's table
-      LdsOrWriter wr{mine, lut, 0, 64 * W};
+      LdsOrWriter<PRIO> wr{mine, lut, 0, 64 * W};
       encode_block<Scalar, DIMS>(f, g.maxbits, wr);
     } else {
       wave_lds_sync();  // the wave's table
-      LdsBitWriter wr{lds, lut, lane * g.maxbits, (lane + 1) * g.maxbits, 0, 0};
+      LdsBitWriter<PRIO> wr{lds, lut, lane * g.maxbits, (lane + 1) * g.maxbits, 0, 0};
       encode_block<Scalar, DIMS>(f, g.maxbits, wr);
     }
   }
-  __builtin_amdgcn_s_setprio(3);  // a wave out of the coder stores at once
+  if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);  // a wave out of the coder stores at once
   wave_lds_sync();
   const uint32_t nb = min((uint32_t)kLanes, g.nblocks - wave * kLanes);
   const uint32_t nwords = (nb * g.maxbits + 63) >> 6;
@@ -468,7 +475,7 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
   ZFP_STAMP_REAL(9);
 }
 
-template <typename Scalar, int DIMS, bool FAST>
+template <typename Scalar, int DIMS, bool FAST, bool PRIO = true>
 __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::value)) void zfp_decode(const uint64_t* __restrict__ stream,
                                                                       Geometry g,
                                                                       Scalar* __restrict__ data) {
@@ -542,20 +549,20 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
     for (uint32_t j = D; j < D + 5; j++) L[j * 64] = 0;
   __syncthreads();
   if (wave >= g.wave_end) return;
-  __builtin_amdgcn_s_setprio(3);  // lowered through the plane loop (progress_priority)
+  if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);  // lowered through the plane loop (progress_priority)
   ZFP_STAMP_HWID();
   ZFP_STAMP_REAL(8);
   ZFP_STAMP(0);
   wave_lds_sync();
   ZFP_STAMP(5);
   if (b < g.nblocks) {
-    LdsReader rd;
+    LdsReader<PRIO> rd;
     rd.lds32 = L;
     rd.lut32 = lut;
     rd.init(0);
     Scalar f[N];
     const bool coded = decode_block<Scalar, DIMS>(f, g.maxbits, rd);
-    __builtin_amdgcn_s_setprio(3);  // a wave out of the coder stores at once
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);  // a wave out of the coder stores at once
     if (coded) {
       scatter<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
     } else {  // a zero block
@@ -579,6 +586,30 @@ static inline uint32_t waves_per_group(uint32_t lds_words, size_t shared_bytes =
   return w;
 }
 
+// The plane-loop priority schedule (progress_priority) when the launch is at
+// most `rounds` resident rounds of waves; without it beyond.  Measured
+// (tools/prio_sweep.sh, profiles/r01_prio_sweep.txt, 3D f32 r8): with the
+// schedule 256^3 (1 round) encode 33.3 / decode 29.7 us vs 35.2 / 33.4 us;
+// 320^3 (1.95 rounds) the decoder still gains (57.5 vs 61.0 us) and the
+// encoder no longer does (62.8 vs 61.3 us); from 384^3 (3.4 rounds) both lose,
+// 768^3 by 14 % of the step.  CUZFP_PRIO=0/1 in the environment forces either.
+static inline bool use_priority(uint32_t nwaves, int waves_per_simd, uint32_t rounds) {
+  static int forced = -2, cus = 0;
+  if (forced == -2) {
+    const char* e = getenv("CUZFP_PRIO");
+    forced = (e && *e) ? (atoi(e) != 0) : -1;
+  }
+  if (forced >= 0) return forced != 0;
+  if (!cus) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;  // MI355X
+    cus = n;
+  }
+  return nwaves <= (uint32_t)cus * 4u * (uint32_t)waves_per_simd * rounds;
+}
+
 template <typename Scalar, int DIMS>
 int launch_encode_t(const void* data, const Geometry& g, bool fast, uint64_t* stream,
                            uint32_t wave0, uint32_t nwaves, hipStream_t st) {
@@ -595,7 +626,9 @@ int launch_encode_t(const void* data, const Geometry& g, bool fast, uint64_t* st
   const dim3 grid((nwaves + wpg - 1) / wpg), block(kLanes * wpg);
   const size_t lds = (size_t)wpg * (gg.lds_words * 8 + kSpreadLutBytes);
   const Scalar* d = (const Scalar*)data;
-  if (fast && aligned)
+  if (fast && aligned && !use_priority(nwaves, occupancy<Scalar, DIMS>::value, 1))
+    hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, true, true, false>), grid, block, lds, st, d, gg, stream);
+  else if (fast && aligned)
     hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, true, true>), grid, block, lds, st, d, gg, stream);
   else if (fast)
     hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, true, false>), grid, block, lds, st, d, gg, stream);
@@ -620,7 +653,9 @@ int launch_decode_t(const uint64_t* stream, const Geometry& g, bool fast, void* 
   const dim3 grid((nwaves + wpg - 1) / wpg), block(kLanes * wpg);
   const size_t lds = (size_t)wpg * gg.lds_words * 8 + kChunkLutBytes;
   Scalar* d = (Scalar*)data;
-  if (fast)
+  if (fast && !use_priority(nwaves, occupancy<Scalar, DIMS>::value, 2))
+    hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, true, false>), grid, block, lds, st, stream, gg, d);
+  else if (fast)
     hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, true>), grid, block, lds, st, stream, gg, d);
   else
     hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, false>), grid, block, lds, st, stream, gg, d);

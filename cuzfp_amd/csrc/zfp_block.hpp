@@ -558,6 +558,20 @@ ZFP_HD bool any_lane(bool p) {
 #define CUZFP_DPRIO_T0 (-1)
 #define CUZFP_DPRIO_AFTER 0
 #endif
+// The schedule pays off when the launch is one resident round of waves (256^3
+// f32: 4 waves per SIMD, all resident at once).  Over several rounds it costs
+// 12 % (1024^3: step 3.63 -> 3.19 ms without it; tools/variants.py): a wave
+// that has lowered its priority is starved by freshly started waves, so the
+// slots it holds free up late.  The launcher picks per launch (kernels.hpp,
+// use_priority), and the coder reads the choice from its writer / reader type
+// (kPrio; types without it keep the schedule).
+template <typename T, typename = void> struct prio_of {
+  static constexpr bool value = true;
+};
+template <typename T> struct prio_of<T, decltype((void)T::kPrio)> {
+  static constexpr bool value = T::kPrio;
+};
+
 template <int T2, int T1, int T0>
 ZFP_HD void progress_priority(int c) {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(CUZFP_NO_PRIO)
@@ -681,7 +695,7 @@ ZFP_HD bool encode_half(const planes<UInt, DIMS>& P, unsigned& n, int cmin, Writ
     if (!any_lane(!wr.full())) return false;
     wr.settle();
     const int u = uniform(c);
-    progress_priority<CUZFP_PRIO_T2, CUZFP_PRIO_T1, CUZFP_PRIO_T0>(u);
+    if constexpr (prio_of<Writer>::value) progress_priority<CUZFP_PRIO_T2, CUZFP_PRIO_T1, CUZFP_PRIO_T0>(u);
     encode_plane_any<DIMS>((PW)P.template get<H>(u), n, wr);
     encode_plane_any<DIMS>((PW)P.template get<H>(u - 1), n, wr);
   }
@@ -1062,7 +1076,8 @@ ZFP_HD int decode_half(planes<UInt, DIMS>& P, unsigned& bits, unsigned& n, int c
   int c = 31;
   for (; c - 1 >= cmin; c -= 2) {
     if (!any_lane(bits != 0)) return c;
-    progress_priority<CUZFP_DPRIO_T2, CUZFP_DPRIO_T1, CUZFP_DPRIO_T0>(uniform(c));
+    if constexpr (prio_of<Reader>::value)
+      progress_priority<CUZFP_DPRIO_T2, CUZFP_DPRIO_T1, CUZFP_DPRIO_T0>(uniform(c));
     const PW xa = decode_plane_any<DIMS, PW>(bits, n, rd);
     const PW xb = decode_plane_any<DIMS, PW>(bits, n, rd);
     const int u = uniform(c);
@@ -1344,7 +1359,7 @@ ZFP_HD bool decode_block(Scalar* f, unsigned maxbits, Reader& rd) {
   planes<UInt, DIMS> P;
   decode_planes<UInt, DIMS>(P, budget, maxprec, rd);
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(CUZFP_NO_PRIO) && CUZFP_DPRIO_AFTER >= 0
-  __builtin_amdgcn_s_setprio(CUZFP_DPRIO_AFTER);  // see progress_priority
+  if constexpr (prio_of<Reader>::value) __builtin_amdgcn_s_setprio(CUZFP_DPRIO_AFTER);  // see progress_priority
 #endif
   ZFP_STAMP(1);
   P.store(u);

@@ -308,3 +308,21 @@ def test_persistent_batches(cuda, restatement, dims, shape, dtype):
         ref = restatement.compress(a, mb)
         assert np.array_equal(words, ref), rate
         assert np.array_equal(y, restatement.decompress(ref, shape, dtype, mb)), rate
+
+
+# --------------------------------------------------------------------------
+# launches of several resident rounds of waves run the kernels without the
+# plane-loop priority schedule (kernels.hpp, use_priority): encoder beyond one
+# round, decoder beyond two (f32: 4,096 waves a round on 256 CUs; 3D f64: 2,048)
+
+
+@pytest.mark.parametrize("shape,dtype,rate", [((576, 256, 256), np.float32, 8),
+                                              ((288, 256, 256), np.float64, 16)])
+def test_multi_round_3d(cuda, restatement, shape, dtype, rate):
+    rng = np.random.default_rng(7)
+    a = _fields(rng, shape, dtype, "smooth")
+    mb = cz.rate_to_maxbits(rate, dtype, 3)
+    words, y = _gpu_roundtrip(a, mb, cuda)
+    ref = restatement.compress(a, mb)
+    assert np.array_equal(words, ref)
+    assert np.array_equal(y, restatement.decompress(ref, shape, dtype, mb))
