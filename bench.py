@@ -56,6 +56,7 @@ def parse():
     p.add_argument("--field", default="polynomial", choices=["polynomial", "splitmix"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-host-path", action="store_true")
+    p.add_argument("--no-copy-probe", action="store_true", help="skip the device-to-device copy bandwidth probe")
     p.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     return p.parse_args()
@@ -83,7 +84,13 @@ def cpu_baseline(a: np.ndarray, maxbits: int):
     rt1, enc1, dec1, _ = ref.time_roundtrip(quarter, maxbits, threads=1, reps=3)
     wall = time.perf_counter() - t0
     nbytes = sample.nbytes
+    model = None
+    try:
+        model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
+    except Exception:  # pragma: no cover
+        pass
     return {"value": round(nbytes / rt / 1e9, 4), "unit": "GB/s", "cores": cores, "kind": kind,
+            "cpu_model": model, "host_cpus_visible": os.cpu_count(),
             "sample": f"the whole {'x'.join(map(str, sample.shape))} {sample.dtype} workload array, maxbits "
                       f"{maxbits}, median of {reps} round trips, slab threads (slowest axis)",
             "encode_GBps": round(nbytes / enc / 1e9, 4), "decode_GBps": round(nbytes / dec / 1e9, 4),
@@ -219,6 +226,31 @@ def main():
     enc_ms = time_kernel(lambda: cz.encode(x, maxbits, out=words), reps)
     dec_ms = time_kernel(lambda: cz.decode(words, shape, x.dtype, maxbits, out=y), reps)
 
+    # achievable HBM bandwidth on this box: a device-to-device copy
+    # (torch's copy kernel, read + write) of the input's size and of 1 GiB
+    def copy_GBps(nbytes):
+        src = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+        dst = torch.empty_like(src)
+        r = graphed(lambda: dst.copy_(src), 10)
+        r()
+        torch.cuda.synchronize()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(3):
+            r()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / 30
+        del src, dst
+        return round(2 * nbytes / (ms * 1e-3) / 1e9, 1)
+
+    hbm_copy = None
+    if rank == 0 and not args.no_copy_probe:
+        hbm_copy = {"kernel": "torch copy_ (device to device)", "GBps_at_input_size": copy_GBps(a.nbytes),
+                    "GBps_1GiB": copy_GBps(1 << 30), "input_bytes": a.nbytes,
+                    "note": "read + write bytes / time, hipGraph of 10 copies"}
+
     # optional RCCL all-gather of the compressed stream (the exchange step)
     allgather = None
     if world > 1 and zd.uniform_shard_ok(gshape, world, maxbits):
@@ -305,7 +337,9 @@ def main():
             "decode_GBps_input": round(n_in / (dec_ms * 1e-3) / 1e9, 1),
             "roofline": {"bound": "hbm", "kernel": f"zfp_{dominant}", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "algorithmic_bytes_per_launch": dom_bytes},
+                         "traffic": traffic, "algorithmic_bytes_per_launch": dom_bytes,
+                         "frac_of_copy": round(achieved / hbm_copy["GBps_1GiB"], 4) if hbm_copy else None},
+            "hbm_copy": hbm_copy,
             "cpu_baseline": cpu,
             "host_path": host_path,
             "allgather": allgather,
