@@ -72,3 +72,62 @@ def test_slab_extent_covers():
             assert spans[0][0] == 0 and spans[-1][1] == n
             for (a0, a1), (b0, b1) in zip(spans, spans[1:]):
                 assert a1 == b0 and (a0 % 4 == 0 or a0 == n)
+
+
+def _gpu_worker(rank, world, port, shape, maxbits, q):
+    # the same path with the HIP kernels: both ranks share cuda:0 (a one-GPU
+    # box), each encodes and decodes its slab on the GPU, the compressed
+    # segments meet through gloo (RCCL needs one GPU per rank)
+    import torch
+    import torch.distributed as dist
+    import cuzfp_amd as cz
+    from cuzfp_amd import dist as zd
+    from cuzfp_amd.datagen import polynomial_slab
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        z0, z1 = zd.slab_extent(shape[0], world, rank)
+        local = polynomial_slab(shape, z0, z1, np.float32)
+        x = torch.from_numpy(local).cuda()
+        words = cz.encode(x, maxbits)
+        y = cz.decode(words, local.shape, x.dtype, maxbits)
+        torch.cuda.synchronize()
+        assert words.numel() == zd.segment_words(shape, world, maxbits)
+        full = zd.allgather_stream(words.cpu())
+        q.put((rank, full.numpy().view(np.uint64).copy(), y.cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_gpu_slabs_allgather(restatement):
+    import multiprocessing as mp
+    import torch
+    from cuzfp_amd import dist as zd
+    from cuzfp_amd.datagen import polynomial_field
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    shape, maxbits, world = (64, 48, 40), 512, 2
+    assert zd.uniform_shard_ok(shape, world, maxbits)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_worker, args=(r, world, port, shape, maxbits, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    for _ in range(world):
+        r, full, y = q.get(timeout=240)
+        results[r] = (full, y)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    a = polynomial_field(shape, np.float32)
+    want = restatement.compress(a, maxbits)
+    back = restatement.decompress(want, shape, np.float32, maxbits)
+    for r in range(world):
+        assert np.array_equal(results[r][0], want)
+        z0, z1 = zd.slab_extent(shape[0], world, r)
+        assert np.array_equal(results[r][1], back[z0:z1])
