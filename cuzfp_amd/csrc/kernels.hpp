@@ -233,6 +233,29 @@ struct LdsReader {
   }
 };
 
+// maxbits <= 64 (1D rate <= 16, 2D rate <= 4: BASELINE's 2D 8192^2 rate 2 and
+// 1D rate 8): the lane's whole block is one 64-bit register, zero past
+// maxbits, read straight from HBM.  The windows are shifts of it, so a plane
+// step waits on one LDS round trip (the chunk tables) instead of two, and
+// there is no LDS stream image to fill.
+template <bool PRIO = true>
+struct RegReader : LdsReader<PRIO> {
+  uint64_t blk;
+  __device__ __forceinline__ uint64_t at(uint32_t p) const { return p < 64 ? blk >> p : 0ull; }
+  __device__ __forceinline__ void windows(uint32_t m, uint64_t& w, uint32_t& g) const {
+    w = at(this->pos);
+    g = (uint32_t)at(this->pos + m);
+  }
+  __device__ __forceinline__ uint64_t peek() const { return at(this->pos); }
+  __device__ __forceinline__ void peek2(uint64_t& a, uint64_t& b) const {
+    a = at(this->pos);
+    b = 0;  // bits past 64: past the block
+  }
+  __device__ __forceinline__ void load() {}
+  __device__ __forceinline__ void init(uint32_t bitpos) { this->pos = bitpos; }
+  __device__ __forceinline__ void skip(unsigned n) { this->pos += n; }
+};
+
 // ---------------------------------------------------------------------------
 // Gather / scatter of one block.  FAST: contiguous layout, every extent a
 // multiple of 4 and a 16-byte aligned base, so each row of 4 values is one
@@ -475,7 +498,7 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
   ZFP_STAMP_REAL(9);
 }
 
-template <typename Scalar, int DIMS, bool FAST, bool PRIO = true>
+template <typename Scalar, int DIMS, bool FAST, bool PRIO = true, bool REG = false>
 __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::value)) void zfp_decode(const uint64_t* __restrict__ stream,
                                                                       Geometry g,
                                                                       Scalar* __restrict__ data) {
@@ -494,59 +517,77 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
   // to 16 to a bank).  Rows D .. D+4 are zero slack for the reader.  The
   // block's loads are issued first, then the workgroup's copy of the chunk
   // tables, so both latencies overlap before the one barrier.
-  const uint32_t D = (g.maxbits + 31) >> 5;  // dwords per block
-  uint32_t* L = (uint32_t*)lds + lane;
-  const uint32_t* seg = (const uint32_t*)(stream + (size_t)wave * g.maxbits);
-  const bool vec = (g.maxbits & 127) == 0 && g.vec_io;
-  constexpr uint32_t kHeld = 8;  // 16-byte pieces held in registers (maxbits <= 1024)
-  uint4 held[kHeld];
-  if (live && vec) {
-    const uint4* src = (const uint4*)(seg + lane * D);
-#pragma unroll
-    for (uint32_t q = 0; q < kHeld; q++)
-      if (4 * q < D) held[q] = src[q];
-  }
   uint32_t* lut = (uint32_t*)(lds_all + (size_t)(blockDim.x >> 6) * g.lds_words);
   // (1D reads chunk-1 entries only: state 2 and the no-group entry)
   constexpr uint32_t kLutFrom = DIMS == 1 ? (2u << kChunkBits) / 4 : 0;
-  for (uint32_t i = kLutFrom + threadIdx.x; i < sizeof(ChunkLut) / 16; i += blockDim.x)
-    ((uint4*)lut)[i] = ((const uint4*)g_chunk_lut.e)[i];
-  if (live) {
-    if (vec) {
-#pragma unroll
-      for (uint32_t q = 0; q < kHeld; q++)
-        if (4 * q < D) {
-          L[(4 * q) * 64] = held[q].x;
-          L[(4 * q + 1) * 64] = held[q].y;
-          L[(4 * q + 2) * 64] = held[q].z;
-          L[(4 * q + 3) * 64] = held[q].w;
-        }
-      const uint4* src = (const uint4*)(seg + lane * D);
-      for (uint32_t q = 4 * kHeld; q < D; q += 4) {  // larger blocks
-        const uint4 v = src[q >> 2];
-        L[q * 64] = v.x;
-        L[(q + 1) * 64] = v.y;
-        L[(q + 2) * 64] = v.z;
-        L[(q + 3) * 64] = v.w;
-      }
-    } else {
-      // the block starts at bit lane*maxbits of the wave's segment; dwords
-      // past the segment's last one read as zero
+  const uint32_t* seg = (const uint32_t*)(stream + (size_t)wave * g.maxbits);
+  uint32_t* L = (uint32_t*)lds + lane;
+  uint64_t blk = 0;
+  if constexpr (REG) {
+    // bits [s0, s0 + maxbits) of the wave's segment; dwords past its last one
+    // read as zero
+    if (live) {
       const uint32_t nb = min((uint32_t)kLanes, g.nblocks - wave * kLanes);
       const uint32_t lim = ((nb * g.maxbits + 63) >> 6) * 2;
       const uint32_t s0 = lane * g.maxbits, d0 = s0 >> 5;
-      uint32_t prev = seg[d0];
-      for (uint32_t j = 0; j < D; j++) {
-        const uint32_t nxt = d0 + j + 1 < lim ? seg[d0 + j + 1] : 0u;
-        L[j * 64] = __builtin_amdgcn_alignbit(nxt, prev, s0);
-        prev = nxt;
-      }
-      // the block reads as zeros past its last bit (decode_plane_lut relies on it)
-      if (g.maxbits & 31) L[(D - 1) * 64] &= (1u << (g.maxbits & 31)) - 1u;
+      const uint32_t a0 = seg[d0];
+      const uint32_t a1 = d0 + 1 < lim ? seg[d0 + 1] : 0u;
+      const uint32_t a2 = d0 + 2 < lim ? seg[d0 + 2] : 0u;
+      blk = ((uint64_t)__builtin_amdgcn_alignbit(a1, a0, s0) |
+             ((uint64_t)__builtin_amdgcn_alignbit(a2, a1, s0) << 32)) & lowmask(g.maxbits);
     }
+    for (uint32_t i = kLutFrom + threadIdx.x; i < sizeof(ChunkLut) / 16; i += blockDim.x)
+      ((uint4*)lut)[i] = ((const uint4*)g_chunk_lut.e)[i];
+  } else {
+    const uint32_t D = (g.maxbits + 31) >> 5;  // dwords per block
+    const bool vec = (g.maxbits & 127) == 0 && g.vec_io;
+    constexpr uint32_t kHeld = 8;  // 16-byte pieces held in registers (maxbits <= 1024)
+    uint4 held[kHeld];
+    if (live && vec) {
+      const uint4* src = (const uint4*)(seg + lane * D);
+#pragma unroll
+      for (uint32_t q = 0; q < kHeld; q++)
+        if (4 * q < D) held[q] = src[q];
+    }
+    for (uint32_t i = kLutFrom + threadIdx.x; i < sizeof(ChunkLut) / 16; i += blockDim.x)
+      ((uint4*)lut)[i] = ((const uint4*)g_chunk_lut.e)[i];
+    if (live) {
+      if (vec) {
+#pragma unroll
+        for (uint32_t q = 0; q < kHeld; q++)
+          if (4 * q < D) {
+            L[(4 * q) * 64] = held[q].x;
+            L[(4 * q + 1) * 64] = held[q].y;
+            L[(4 * q + 2) * 64] = held[q].z;
+            L[(4 * q + 3) * 64] = held[q].w;
+          }
+        const uint4* src = (const uint4*)(seg + lane * D);
+        for (uint32_t q = 4 * kHeld; q < D; q += 4) {  // larger blocks
+          const uint4 v = src[q >> 2];
+          L[q * 64] = v.x;
+          L[(q + 1) * 64] = v.y;
+          L[(q + 2) * 64] = v.z;
+          L[(q + 3) * 64] = v.w;
+        }
+      } else {
+        // the block starts at bit lane*maxbits of the wave's segment; dwords
+        // past the segment's last one read as zero
+        const uint32_t nb = min((uint32_t)kLanes, g.nblocks - wave * kLanes);
+        const uint32_t lim = ((nb * g.maxbits + 63) >> 6) * 2;
+        const uint32_t s0 = lane * g.maxbits, d0 = s0 >> 5;
+        uint32_t prev = seg[d0];
+        for (uint32_t j = 0; j < D; j++) {
+          const uint32_t nxt = d0 + j + 1 < lim ? seg[d0 + j + 1] : 0u;
+          L[j * 64] = __builtin_amdgcn_alignbit(nxt, prev, s0);
+          prev = nxt;
+        }
+        // the block reads as zeros past its last bit (decode_plane_lut relies on it)
+        if (g.maxbits & 31) L[(D - 1) * 64] &= (1u << (g.maxbits & 31)) - 1u;
+      }
+    }
+    if (wave < g.wave_end)
+      for (uint32_t j = D; j < D + 5; j++) L[j * 64] = 0;
   }
-  if (wave < g.wave_end)
-    for (uint32_t j = D; j < D + 5; j++) L[j * 64] = 0;
   __syncthreads();
   if (wave >= g.wave_end) return;
   if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);  // lowered through the plane loop (progress_priority)
@@ -556,12 +597,22 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
   wave_lds_sync();
   ZFP_STAMP(5);
   if (b < g.nblocks) {
-    LdsReader<PRIO> rd;
-    rd.lds32 = L;
-    rd.lut32 = lut;
-    rd.init(0);
     Scalar f[N];
-    const bool coded = decode_block<Scalar, DIMS>(f, g.maxbits, rd);
+    bool coded;
+    if constexpr (REG) {
+      RegReader<PRIO> rd;
+      rd.lds32 = L;
+      rd.lut32 = lut;
+      rd.blk = blk;
+      rd.init(0);
+      coded = decode_block<Scalar, DIMS>(f, g.maxbits, rd);
+    } else {
+      LdsReader<PRIO> rd;
+      rd.lds32 = L;
+      rd.lut32 = lut;
+      rd.init(0);
+      coded = decode_block<Scalar, DIMS>(f, g.maxbits, rd);
+    }
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);  // a wave out of the coder stores at once
     if (coded) {
       scatter<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
@@ -649,10 +700,29 @@ int launch_decode_t(const uint64_t* stream, const Geometry& g, bool fast, void* 
   gg.wave_end = wave0 + nwaves;
   gg.vec_io = (g.maxbits % 2 == 0) && ((uintptr_t)stream % 16 == 0);
   gg.lds_words = ((g.maxbits + 31) / 32 + 5) * 32;  // (dwords per block + 5 slack rows) x 64 lanes
+  // blocks of at most 64 bits are read into registers (RegReader): no LDS image
+  const bool reg = DIMS <= 2 && g.maxbits <= 64;
+  if (reg) gg.lds_words = 0;
   const uint32_t wpg = waves_per_group(gg.lds_words, kChunkLutBytes);
   const dim3 grid((nwaves + wpg - 1) / wpg), block(kLanes * wpg);
   const size_t lds = (size_t)wpg * gg.lds_words * 8 + kChunkLutBytes;
   Scalar* d = (Scalar*)data;
+  if constexpr (DIMS <= 2) {
+    if (reg) {
+      const bool prio = use_priority(nwaves, occupancy<Scalar, DIMS>::value, 2);
+      if (fast && prio)
+        hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, true, true, true>), grid, block, lds, st, stream, gg, d);
+      else if (fast)
+        hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, true, false, true>), grid, block, lds, st, stream, gg, d);
+      else if (prio)
+        hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, false, true, true>), grid, block, lds, st, stream, gg, d);
+      else
+        hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, false, false, true>), grid, block, lds, st, stream, gg, d);
+      const hipError_t e = hipGetLastError();
+      t_last_hip = e;
+      return e == hipSuccess ? CUZFP_SUCCESS : CUZFP_ERROR_HIP;
+    }
+  }
   if (fast && !use_priority(nwaves, occupancy<Scalar, DIMS>::value, 2))
     hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, true, false>), grid, block, lds, st, stream, gg, d);
   else if (fast)
