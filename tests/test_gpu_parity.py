@@ -326,3 +326,36 @@ def test_multi_round_3d(cuda, restatement, shape, dtype, rate):
     ref = restatement.compress(a, mb)
     assert np.array_equal(words, ref)
     assert np.array_equal(y, restatement.decompress(ref, shape, dtype, mb))
+
+
+# --------------------------------------------------------------------------
+# blocks of at most 64 bits take the register reader (kernels.hpp, RegReader):
+# every such maxbits class in 1D/2D, random streams of several densities and
+# encoded fields, multi-wave arrays with a partial last wave
+
+
+@pytest.mark.parametrize("dims", [1, 2])
+@pytest.mark.parametrize("dtype", [np.float32, np.float64, np.int32])
+def test_register_reader(cuda, restatement, dims, dtype):
+    import torch
+    rng = np.random.default_rng(101 + dims + 7 * np.dtype(dtype).itemsize)
+    tdt = {np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64,
+           np.dtype(np.int32): torch.int32}[np.dtype(dtype)]
+    shape = (4 * 64 * 5 + 9,) if dims == 1 else (90, 75)
+    for mb in (9, 12, 13, 17, 31, 32, 33, 47, 48, 63, 64):
+        if mb < (9 if np.dtype(dtype).itemsize == 4 else 12):
+            continue
+        nb = int(np.prod([(s + 3) // 4 for s in shape]))
+        words = (nb * mb + 63) // 64
+        for density in (0.5, 0.05, 0.95):
+            bits = rng.random(words * 64) < density
+            s = np.packbits(bits.reshape(-1, 8)[:, ::-1], axis=1).reshape(-1).view(np.uint64).copy()
+            want = restatement.decompress(s, shape, dtype, mb)
+            got = cz.decode(torch.from_numpy(s.view(np.int64)).to(cuda), shape, tdt, mb).cpu().numpy()
+            assert np.array_equal(got.view(np.uint8), want.view(np.uint8)), (mb, density)
+        if np.dtype(dtype).kind == "f":
+            a = _fields(rng, shape, dtype, "smooth")
+            w, y = _gpu_roundtrip(a, mb, cuda)
+            ref = restatement.compress(a, mb)
+            assert np.array_equal(w, ref), mb
+            assert np.array_equal(y.view(np.uint8), restatement.decompress(ref, shape, dtype, mb).view(np.uint8)), mb
