@@ -668,6 +668,8 @@ ZFP_HD bool encode_plane_lut(PW x, unsigned& n, Writer& wr) {
   return true;
 }
 
+// general plane step: the two-put table coder, or the exact group coder for
+// a dense plane
 template <int DIMS, typename PW, typename Writer>
 ZFP_HD void encode_plane_any(PW x, unsigned& n, Writer& wr) {
   // one wave-uniform test: the per-lane branch around the table coder costs
@@ -685,6 +687,68 @@ ZFP_HD void encode_plane_any(PW x, unsigned& n, Writer& wr) {
   }
 }
 
+// v_bfe_u32(v, 0, w): the low w bits of v, w = 0 .. 31
+ZFP_HD uint32_t low_bits(uint32_t v, uint32_t w) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_ubfe(v, 0u, w);
+#else
+  return w ? v & (0xffffffffu >> (32 - (w & 31))) : 0u;
+#endif
+}
+
+// One-put plane step (the common case).  The whole plane code -- n verbatim
+// bits, then the group code -- goes out with one writer call when it fits 64
+// bits.  With r = x >> n the code is x ^ ((r ^ g) << n), g = the group code:
+// "1", then r with every one doubled (Writer::spread), cut before the top
+// one's partner (the closing "0", which the zeroed image already holds), i.e.
+// the low L = bitlen(r) + popcount(r) bits of (spread(r) << 1 | 1) -- or, when
+// r's top one lands on position N-1 (imp: it is implied), the low L - 1 bits
+// and no closing test.  No new ones: L = 0, g = 0 and the single "0" test.
+// n is kept at most N-1: with n = N-1 the last position's code is its bit
+// alone either way (a "1" test with the one implied, or a "0" test), so the
+// plane codes are those of n = N, verbatim.  Requires width <= 31, which
+// holds for r < 2^15 (3D: checked by the caller) and always in 1D/2D.
+template <int DIMS, typename PW, typename Writer>
+ZFP_HD void encode_plane_one_put(PW x, unsigned nf, uint32_t rl, uint32_t bl, uint32_t L, unsigned& n,
+                                 Writer& wr) {
+  constexpr unsigned N = 1u << (2 * DIMS);
+  const uint32_t nn = nf + bl;           // <= N
+  const uint32_t imp = nn >> (2 * DIMS);  // r's top one at N-1
+  const uint32_t width = L - imp;
+  const uint32_t len = nf + width + 1u - imp;
+  const uint32_t b0 = rl & 0xffu;
+  const uint32_t E = N <= 4 ? wr.spread(b0)
+                            : wr.spread(b0) | (wr.spread(rl >> 8) << (uint32_t)(__builtin_popcount(b0) + 8));
+  const uint32_t g = low_bits((E << 1) | 1u, width);
+  const uint64_t code = (uint64_t)x ^ ((uint64_t)(rl ^ g) << nf);
+  wr.put(code, len);
+  n = nn < N - 1 ? nn : N - 1;
+}
+
+template <int DIMS, typename PW, typename Writer>
+ZFP_HD void encode_plane_step(PW x, unsigned& n, Writer& wr) {
+  constexpr unsigned N = 1u << (2 * DIMS);
+  const unsigned nf = n < N - 1 ? n : N - 1;
+  const uint64_t r = (uint64_t)x >> nf;
+  const uint32_t rl = (uint32_t)r;
+  const uint32_t bl = bitlen16(rl);                           // exact for r < 2^24
+  const uint32_t L = (uint32_t)__builtin_popcount(rl) + bl;  // v_bcnt_u32_b32(rl, bl)
+  if constexpr (N <= 16) {
+    // r has at most 16 bits and the code at most 48: always one put
+    encode_plane_one_put<DIMS>(x, nf, rl, bl, L, n, wr);
+  } else {
+    // one put while every lane's code fits 64 bits with r < 2^15 (3D rate 8
+    // on smooth data: ~26 of ~29 plane steps, tools/coder_stats.cpp);
+    // otherwise the general step for the whole wave
+    const uint32_t imp = (nf + bl) >> 6;
+    const bool ok = (r >> 15) == 0 && nf + L + 1u - 2u * imp <= 64u;
+    if (__builtin_expect(!any_lane(!ok), 1))
+      encode_plane_one_put<DIMS>(x, nf, rl, bl, L, n, wr);
+    else
+      encode_plane_any<DIMS>(x, n, wr);
+  }
+}
+
 // Planes 31 .. cmin of 32-bit half H, two at a time (an odd one left at the
 // bottom goes alone); false once the block is full.
 template <int H, typename UInt, int DIMS, typename Writer>
@@ -696,13 +760,13 @@ ZFP_HD bool encode_half(const planes<UInt, DIMS>& P, unsigned& n, int cmin, Writ
     wr.settle();
     const int u = uniform(c);
     if constexpr (prio_of<Writer>::value) progress_priority<CUZFP_PRIO_T2, CUZFP_PRIO_T1, CUZFP_PRIO_T0>(u);
-    encode_plane_any<DIMS>((PW)P.template get<H>(u), n, wr);
-    encode_plane_any<DIMS>((PW)P.template get<H>(u - 1), n, wr);
+    encode_plane_step<DIMS>((PW)P.template get<H>(u), n, wr);
+    encode_plane_step<DIMS>((PW)P.template get<H>(u - 1), n, wr);
   }
   if (c >= cmin && c >= 0) {
     if (!any_lane(!wr.full())) return false;
     wr.settle();
-    encode_plane_any<DIMS>((PW)P.template get<H>(uniform(c)), n, wr);
+    encode_plane_step<DIMS>((PW)P.template get<H>(uniform(c)), n, wr);
   }
   return true;
 }
