@@ -8,7 +8,7 @@ memory and streams only.  There is no CPU fallback: every entry point raises
 if the HIP library is missing.
 
 Array shapes are numpy/torch order (slowest first): ``(nx,)``, ``(ny, nx)``,
-``(nz, ny, nx)`` -- the reference's ``a[nz][ny][nx]`` (zfp_structs.h:57).
+``(nz, ny, nx)`` -- the reference's ``a[nz][ny][nx]`` (zfp_structs.h:42).
 """
 from __future__ import annotations
 

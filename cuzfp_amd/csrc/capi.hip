@@ -311,7 +311,7 @@ size_t cuzfp_hip_stream_bytes(int type, unsigned nx, unsigned ny, unsigned nz, u
 }
 
 size_t cuzfp_hip_maximum_size(int type, unsigned nx, unsigned ny, unsigned nz, unsigned maxbits) {
-  // zfp_structs.h:237-266 in fixed-rate mode: minbits == maxbits, so every
+  // zfp_structs.h:222-251 in fixed-rate mode: minbits == maxbits, so every
   // block is exactly maxbits bits; plus the reference's 148-bit header allowance
   Problem p;
   if (make_problem(type, nx, ny, nz, 0, 0, 0, maxbits, &p) != CUZFP_SUCCESS) return 0;

@@ -725,6 +725,59 @@ ZFP_HD void encode_plane_one_put(PW x, unsigned nf, uint32_t rl, uint32_t bl, ui
   n = nn < N - 1 ? nn : N - 1;
 }
 
+// r with every one doubled, for a 32-bit r: four byte lookups placed at
+// 8 i + (ones below byte i); at most 64 bits
+template <typename Writer>
+ZFP_HD uint64_t spread32(uint32_t v, const Writer& wr) {
+  const uint32_t b0 = v & 0xffu, b1 = (v >> 8) & 0xffu, b2 = (v >> 16) & 0xffu, b3 = v >> 24;
+  const uint32_t o1 = (uint32_t)__builtin_popcount(b0) + 8u;
+  const uint32_t o2 = (uint32_t)__builtin_popcount(v & 0xffffu) + 16u;
+  const uint32_t o3 = (uint32_t)__builtin_popcount(v & 0xffffffu) + 24u;
+  const uint32_t s01 = wr.spread(b0) | (wr.spread(b1) << o1);  // < 2^32
+  return (uint64_t)s01 | ((uint64_t)wr.spread(b2) << o2) | ((uint64_t)wr.spread(b3) << o3);
+}
+
+ZFP_HD uint32_t bitlen32(uint32_t x) { return x ? 32u - (uint32_t)__builtin_clz(x) : 0u; }
+
+// General 3D plane step without a loop over the new ones (replaces the
+// one-put step when some lane's code is longer than 64 bits or has new ones
+// past r's 15th bit: dense planes, the last few of a block).  Three puts:
+// the verbatim bits with the leading group test (n + 1 <= 64 bits), then r's
+// doubled form in two halves (r's low and high 32 positions, each <= 64
+// bits), the top one's partner dropped and the closing "0" counted (imp: the
+// top one dropped too and no closing test).  The high half is skipped when no
+// lane of the wave has new ones past position 31.  Bits past the block's
+// budget land in the writer's slack; settle() first bounds them.
+template <typename Writer>
+ZFP_HD void encode_plane_wide(uint64_t x, unsigned& n, Writer& wr) {
+  wr.settle();
+  const unsigned nf = n < 63u ? n : 63u;
+  const uint64_t r = x >> nf;
+  const uint32_t lo = (uint32_t)r, hi = (uint32_t)(r >> 32);
+  const uint32_t blh = bitlen32(hi);
+  const uint32_t bl = blh ? 32u + blh : bitlen32(lo);
+  const uint32_t nn = nf + bl;  // <= 64
+  const uint32_t imp = nn >> 6;
+  const uint64_t nz = r != 0 ? 1u : 0u;
+  wr.put((x ^ (r << nf)) | (nz << nf), nf + 1u);  // verbatim bits, then "1" (new ones) or "0"
+  const uint64_t slo = spread32(lo, wr);
+  const uint32_t tlo = (uint32_t)__builtin_popcount(lo);
+  uint64_t top = slo;
+  uint32_t ltop = bl + tlo;  // bits of the doubled form in the top part
+  if (__builtin_expect(any_lane(hi != 0), 0)) {
+    const uint64_t shi = spread32(hi, wr);
+    // hi != 0: the low half is whole (32 positions, 32 + tlo bits) and the
+    // top part is the high half
+    wr.put(hi ? slo : 0ull, hi ? 32u + tlo : 0u);
+    top = hi ? shi : slo;
+    ltop = hi ? blh + (uint32_t)__builtin_popcount(hi) : ltop;
+  }
+  // drop the top one's partner (imp: the top one too); ltop >= 2 when r != 0
+  const uint64_t cut = nz ? (uint64_t)(2u + imp) << ((ltop - 2u) & 63) : 0ull;
+  wr.put(top & ~cut, ltop - 2u * imp);  // + the closing "0" (unless imp)
+  n = nn < 63u ? nn : 63u;
+}
+
 template <int DIMS, typename PW, typename Writer>
 ZFP_HD void encode_plane_step(PW x, unsigned& n, Writer& wr) {
   constexpr unsigned N = 1u << (2 * DIMS);
@@ -739,13 +792,13 @@ ZFP_HD void encode_plane_step(PW x, unsigned& n, Writer& wr) {
   } else {
     // one put while every lane's code fits 64 bits with r < 2^15 (3D rate 8
     // on smooth data: ~26 of ~29 plane steps, tools/coder_stats.cpp);
-    // otherwise the general step for the whole wave
+    // otherwise the wide step for the whole wave
     const uint32_t imp = (nf + bl) >> 6;
     const bool ok = (r >> 15) == 0 && nf + L + 1u - 2u * imp <= 64u;
     if (__builtin_expect(!any_lane(!ok), 1))
       encode_plane_one_put<DIMS>(x, nf, rl, bl, L, n, wr);
     else
-      encode_plane_any<DIMS>(x, n, wr);
+      encode_plane_wide((uint64_t)x, n, wr);
   }
 }
 

@@ -19,8 +19,8 @@
  *                        decode2.cuh:141-182, decode3.cuh:217-264).
  *   cuzfp_hip_stream_bytes <- the byte count those launchers return
  *                        (calc_device_mem{1,2,3}d, e.g. encode3.cuh:413-423).
- *   cuzfp_hip_maximum_size <- zfp_stream_maximum_size (zfp_structs.h:237-266).
- *   cuzfp_hip_rate_to_maxbits <- stream_set_rate (zfp_structs.h:61-91).
+ *   cuzfp_hip_maximum_size <- zfp_stream_maximum_size (zfp_structs.h:222-251).
+ *   cuzfp_hip_rate_to_maxbits <- stream_set_rate (zfp_structs.h:46-76).
  *   cuzfp_hip_compress_host / cuzfp_hip_decompress_host <- the host-pointer
  *                        staging of cuZFP::compress / decompress
  *                        (cuZFP.cu:107-170, 174-269), as a pinned, chunked,
@@ -50,7 +50,7 @@ extern "C" {
 
 #define CUZFP_HIP_ABI_VERSION 1
 
-/* scalar type codes: the reference's zfp_type enum (zfp_structs.h:46-52) */
+/* scalar type codes: the reference's zfp_type enum (zfp_structs.h:31-37) */
 #define CUZFP_TYPE_INT32 1
 #define CUZFP_TYPE_INT64 2
 #define CUZFP_TYPE_FLOAT 3

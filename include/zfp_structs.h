@@ -21,14 +21,14 @@
 #define ZFP_HEADER_MAX_BITS 148  /* max number of header bits */
 
 typedef unsigned int uint;
-typedef unsigned long long Word;  // stream word (zfp_structs.h:31)
+typedef unsigned long long Word;  // stream word (zfp_structs.h:16)
 #ifndef wsize
 #define wsize ((uint)(CHAR_BIT * sizeof(Word)))
 #endif
 
 namespace cuZFP {
 
-// zfp_structs.h:37-44 -- only maxbits is used by the fixed-rate codec
+// zfp_structs.h:22-29 -- only maxbits is used by the fixed-rate codec
 typedef struct {
   uint minbits;
   uint maxbits;
@@ -37,7 +37,7 @@ typedef struct {
   Word* stream;  // host or device pointer to the compressed words
 } zfp_stream;
 
-// zfp_structs.h:46-52
+// zfp_structs.h:31-37
 typedef enum {
   zfp_type_none = 0,
   zfp_type_int32 = 1,
@@ -46,7 +46,7 @@ typedef enum {
   zfp_type_double = 4
 } zfp_type;
 
-// zfp_structs.h:54-59.  Unlike the reference, which ignores sx/sy/sz
+// zfp_structs.h:39-44.  Unlike the reference, which ignores sx/sy/sz
 // (SURVEY.md 8a row a1), non-zero strides are honoured as in CPU zfp.
 typedef struct {
   zfp_type type;
@@ -55,7 +55,7 @@ typedef struct {
   void* data;
 } zfp_field;
 
-// zfp_structs.h:61-91: bits/block = floor(4^d * rate + 0.5), at least
+// zfp_structs.h:46-76: bits/block = floor(4^d * rate + 0.5), at least
 // 1 + exponent bits; 3D rounded up to a multiple of 64 (as the reference does).
 static double stream_set_rate(zfp_stream* zfp, double rate, zfp_type type, uint dims) {
   const uint n = 1u << (2 * dims);
@@ -145,7 +145,7 @@ static size_t zfp_type_size(zfp_type type) {
   }
 }
 
-// zfp_structs.h:237-266: worst-case stream bytes for `field` under `zfp`.
+// zfp_structs.h:222-251: worst-case stream bytes for `field` under `zfp`.
 static size_t zfp_stream_maximum_size(const zfp_stream* zfp, const zfp_field* field) {
   const uint dims = zfp_field_dimensionality(field);
   if (!dims || field->type == zfp_type_none) return 0;

@@ -30,14 +30,16 @@ int main(int argc, char** argv) {
   // per-plane-step histograms (step = plane index from the top, 0..31)
   long lanes_active[32] = {0}, r_zero[32] = {0}, n_full[32] = {0}, r_wide[32] = {0};
   long wave_all_r0[32] = {0}, wave_any_active[32] = {0}, wave_any_wide[32] = {0}, wave_all_full[32] = {0};
-  long wave_fit64[32] = {0};
+  long wave_fit64[32] = {0}, wave_g20[32] = {0}, wave_g40[32] = {0}, wave_g60[32] = {0};
   long planes_hist[33] = {0}, wave_steps_hist[33] = {0};
   long sum_planes = 0, sum_wave_steps = 0;
+  long slow_rem[26] = {0}, slow_n[65] = {0}, slow_len[16] = {0}, slow_fits_budget = 0, slow_total = 0;
   uint64_t st = 42;
   const size_t nwaves = (blocks + 63) / 64;
   for (size_t w = 0; w < nwaves; w++) {
     int wsteps = 0;
     bool act[64][32] = {}, rz[64][32] = {}, wide[64][32] = {}, full[64][32] = {}, fit[64][32] = {};
+    unsigned glen[64][32] = {};
     for (int l = 0; l < 64; l++) {
       const size_t b = w * 64 + l;
       if (b >= blocks) break;
@@ -66,6 +68,7 @@ int main(int argc, char** argv) {
       int k = 0;
       for (; k < 32 && bits; k++) {
         const uint64_t x = P.get(31 - k);
+        const unsigned nn0 = nn;
         const uint64_t r = nn < 64 ? x >> nn : 0;
         act[l][k] = true;
         rz[l][k] = r == 0;
@@ -82,6 +85,15 @@ int main(int argc, char** argv) {
           }
         }
         fit[l][k] = len <= 64;
+        glen[l][k] = len - nn0;
+        if (!(r >> 15 == 0 && len <= 64)) {
+          const unsigned rem = bits;
+          slow_rem[rem > 200 ? 200 / 8 : rem / 8]++;
+          slow_n[nn0 > 64 ? 64 : nn0]++;
+          slow_len[len > 127 ? 15 : len / 8]++;
+          slow_fits_budget += rem <= 64;
+          slow_total++;
+        }
         bits = len >= bits ? 0 : bits - len;
       }
       sum_planes += k;
@@ -92,6 +104,7 @@ int main(int argc, char** argv) {
     wave_steps_hist[wsteps]++;
     for (int k = 0; k < wsteps; k++) {
       bool all0 = true, anyw = false, allf = true, allfit = true;
+      unsigned gmax = 0;
       for (int l = 0; l < 64; l++) {
         if (act[l][k]) {
           lanes_active[k]++;
@@ -102,6 +115,7 @@ int main(int argc, char** argv) {
           anyw |= wide[l][k];
           allf &= full[l][k];
           allfit &= fit[l][k];
+          if (glen[l][k] > gmax) gmax = glen[l][k];
         }
       }
       wave_any_active[k]++;
@@ -109,23 +123,35 @@ int main(int argc, char** argv) {
       wave_any_wide[k] += anyw;
       wave_all_full[k] += allf;
       wave_fit64[k] += allfit;
+      wave_g20[k] += gmax > 20;
+      wave_g40[k] += gmax > 40;
+      wave_g60[k] += gmax > 60;
     }
   }
   printf("blocks %zu waves %zu: planes per block mean %.2f, wave steps mean %.2f\n", blocks, nwaves,
          (double)sum_planes / blocks, (double)sum_wave_steps / nwaves);
-  printf("step lanes_act%%  r==0%%  n==64%%  r>=2^16%% | waves: steps  all_r0%%  any_wide%%  all_full%%  all_fit64%%\n");
+  printf("step lanes_act%%  r==0%%  n==64%%  r>=2^16%% | waves: steps  all_r0%%  any_wide%%  all_full%%  all_fit64%%  grp>20%% grp>40%% grp>60%%\n");
   for (int k = 0; k < 32; k++) {
     if (!wave_any_active[k]) break;
     const double la = lanes_active[k];
-    printf("%3d %8.1f %7.1f %7.1f %8.2f | %7ld %7.1f %8.2f %8.1f %8.1f\n", k, 100.0 * la / (wave_any_active[k] * 64.0),
+    printf("%3d %8.1f %7.1f %7.1f %8.2f | %7ld %7.1f %8.2f %8.1f %8.1f %7.1f %7.1f %7.1f\n", k, 100.0 * la / (wave_any_active[k] * 64.0),
            100.0 * r_zero[k] / la, 100.0 * n_full[k] / la, 100.0 * r_wide[k] / la, wave_any_active[k],
            100.0 * wave_all_r0[k] / wave_any_active[k], 100.0 * wave_any_wide[k] / wave_any_active[k],
-           100.0 * wave_all_full[k] / wave_any_active[k], 100.0 * wave_fit64[k] / wave_any_active[k]);
+           100.0 * wave_all_full[k] / wave_any_active[k], 100.0 * wave_fit64[k] / wave_any_active[k], 100.0 * wave_g20[k] / wave_any_active[k],
+           100.0 * wave_g40[k] / wave_any_active[k], 100.0 * wave_g60[k] / wave_any_active[k]);
   }
   printf("planes-per-block histogram:");
   for (int k = 0; k <= 32; k++) if (planes_hist[k]) printf(" %d:%ld", k, planes_hist[k]);
   printf("\nwave-steps histogram:");
   for (int k = 0; k <= 32; k++) if (wave_steps_hist[k]) printf(" %d:%ld", k, wave_steps_hist[k]);
+  printf("\n");
+  printf("slow lane-steps %ld, remaining budget <= 64: %.1f%%\n", slow_total, 100.0 * slow_fits_budget / (slow_total ? slow_total : 1));
+  printf("slow: remaining budget hist (8-bit bins):");
+  for (int i = 0; i < 26; i++) if (slow_rem[i]) printf(" %d:%ld", i * 8, slow_rem[i]);
+  printf("\nslow: n hist:");
+  for (int i = 0; i <= 64; i++) if (slow_n[i]) printf(" %d:%ld", i, slow_n[i]);
+  printf("\nslow: code len hist (8-bit bins):");
+  for (int i = 0; i < 16; i++) if (slow_len[i]) printf(" %d:%ld", i * 8, slow_len[i]);
   printf("\n");
   return 0;
 }

@@ -20,6 +20,13 @@ for s in $STEPS; do
     pytest)
       timeout -k 10 1200 python -m pytest tests -m gpu -x -q -p no:cacheprovider > "$OUT/pytest_gpu_$TAG.log" 2>&1
       ok_or_stop $? pytest; tail -5 "$OUT/pytest_gpu_$TAG.log" ;;
+    quick)
+      # the parity subset that exercises every coder path (golden BASELINE streams, fuzz, extremes, random streams)
+      timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -m gpu -x -q -p no:cacheprovider -k "golden_baseline or fuzz_vs_oracle or extreme or random_streams or golden_fuzz" > "$OUT/pytest_quick_$TAG.log" 2>&1
+      ok_or_stop $? quick; tail -3 "$OUT/pytest_quick_$TAG.log" ;;
+    benchq)
+      timeout -k 10 300 python bench.py --no-cpu-baseline --no-host-path > "$OUT/benchq_$TAG.json" 2> "$OUT/benchq_$TAG.err"
+      ok_or_stop $? benchq; python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('value', d['value'], 'enc', d['encode_ms'], 'dec', d['decode_ms'], d['parity'])" "$OUT/benchq_$TAG.json" ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke_$TAG.log" 2>&1
       ok_or_stop $? smoke; tail -2 "$OUT/smoke_$TAG.log" ;;
