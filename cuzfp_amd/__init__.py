@@ -144,6 +144,22 @@ def _strides(x):
     return st[0], st[1] if x.dim() > 1 else 0, st[2] if x.dim() > 2 else 0
 
 
+def _broadcast(x) -> bool:
+    """True for a view with a zero stride on an axis of extent > 1 (expand /
+    broadcast): the C-ABI reads a zero stride as "contiguous default", so such
+    a view must not be passed through as it is."""
+    return any(st == 0 and n > 1 for st, n in zip(x.stride(), x.shape))
+
+
+def _check_host_out(out: np.ndarray, shape, dtype, what: str) -> None:
+    if not isinstance(out, np.ndarray) or not out.flags.c_contiguous:
+        raise ValueError(f"{what}: out must be a C-contiguous numpy array")
+    if out.dtype != np.dtype(dtype):
+        raise ValueError(f"{what}: out has dtype {out.dtype}, expected {np.dtype(dtype)}")
+    if shape is not None and tuple(out.shape) != tuple(int(s) for s in shape):
+        raise ValueError(f"{what}: out has shape {out.shape}, expected {tuple(shape)}")
+
+
 def encode(x, maxbits: int, out=None, stream=None):
     """Compress a CUDA tensor; returns the stream as an int64 tensor of 64-bit words.
 
@@ -153,6 +169,8 @@ def encode(x, maxbits: int, out=None, stream=None):
     import torch
     if not x.is_cuda:
         raise ValueError("encode: expects a device tensor (use compress_host for host arrays)")
+    if _broadcast(x):
+        x = x.contiguous()  # materialise a broadcast view (a zero stride means "contiguous" to the C-ABI)
     t = type_code(x.dtype)
     nx, ny, nz = _extents(x.shape)
     nbytes = stream_bytes(x.shape, x.dtype, maxbits)
@@ -174,6 +192,8 @@ def decode(words, shape, dtype, maxbits: int, out=None, stream=None):
         raise ValueError("decode: expects a device stream")
     if out is None:
         out = torch.empty(tuple(shape), dtype=dtype, device=words.device)
+    elif _broadcast(out):
+        raise ValueError("decode: out is a broadcast view (zero stride); its elements alias each other")
     t = type_code(out.dtype)
     nx, ny, nz = _extents(out.shape)
     sx, sy, sz = _strides(out)
@@ -191,6 +211,10 @@ def compress_host(a: np.ndarray, maxbits: int, nstreams: int = 2, out: np.ndarra
     nbytes = stream_bytes(a.shape, a.dtype, maxbits)
     if out is None:
         out = np.empty(nbytes // 8, dtype=np.uint64)
+    else:
+        _check_host_out(out, None, out.dtype, "compress_host")
+        if out.nbytes < nbytes:
+            raise ValueError(f"compress_host: out holds {out.nbytes} bytes, the stream needs {nbytes}")
     got = ctypes.c_size_t(0)
     rc = library().cuzfp_hip_compress_host(a.ctypes.data, type_code(a.dtype), nx, ny, nz, maxbits,
                                            out.ctypes.data, out.nbytes, ctypes.byref(got), nstreams)
@@ -203,6 +227,8 @@ def decompress_host(words: np.ndarray, shape, dtype, maxbits: int, nstreams: int
     words = np.ascontiguousarray(words)
     if out is None:
         out = np.empty(tuple(shape), dtype=dtype)
+    else:
+        _check_host_out(out, shape, dtype, "decompress_host")
     nx, ny, nz = _extents(out.shape)
     rc = library().cuzfp_hip_decompress_host(words.ctypes.data, words.nbytes, type_code(out.dtype),
                                              nx, ny, nz, maxbits, out.ctypes.data, nstreams)

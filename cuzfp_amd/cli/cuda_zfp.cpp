@@ -360,6 +360,7 @@ int main(int argc, char** argv) {
     fill_field(field, raw_out.data());
     zfp.stream = words.data();
     cuZFP::decompress(&zfp, &field);
+    if (cuZFP_last_status()) return fail("decompression failed");
     if (outpath && !write_all(outpath, raw_out.data(), raw_out.size())) return fail("cannot write output file");
   }
 

@@ -19,8 +19,12 @@ static int make_problem(int type, unsigned nx, unsigned ny, unsigned nz, long lo
   if (!nx || (nz && !ny)) return CUZFP_ERROR_INVALID_ARGUMENT;
   const unsigned dims = nz ? 3 : ny ? 2 : 1;
   const unsigned ebits = type == CUZFP_TYPE_FLOAT ? 9 : type == CUZFP_TYPE_DOUBLE ? 12 : 1;
-  // LDS image of one wave's segment must fit a workgroup's 64 KiB
-  if (maxbits < ebits || maxbits > 8000) return CUZFP_ERROR_INVALID_ARGUMENT;
+  // One wave's LDS image must fit a workgroup's 64 KiB beside the tables: the
+  // decoder's (maxbits / 32 + 5 rows of 256 B + 12 KiB of chunk tables) up to
+  // maxbits 6,464.  CUZFP_MAX_BITS (6,144) is well above the most bits any
+  // block can use (zfp's ZFP_MAX_BITS, 4,171: 3D double at full precision);
+  // past that a stream is padding.
+  if (maxbits < ebits || maxbits > CUZFP_MAX_BITS) return CUZFP_ERROR_INVALID_ARGUMENT;
   Geometry& g = pr->g;
   g.nx = nx;
   g.ny = dims > 1 ? ny : 1;
@@ -92,6 +96,17 @@ static uint32_t waves_of(const Geometry& g) { return (g.nblocks + kLanes - 1) / 
 
 constexpr size_t kChunkBytes = 32u << 20;
 
+// chunk size: kChunkBytes, or CUZFP_HOST_CHUNK_BYTES from the environment
+// (read per call; tests use small chunks to run the multi-chunk paths)
+static size_t chunk_bytes() {
+  const char* e = getenv("CUZFP_HOST_CHUNK_BYTES");
+  if (e && *e) {
+    const long long v = atoll(e);
+    if (v > 0) return (size_t)v;
+  }
+  return kChunkBytes;
+}
+
 static bool is_pinned_host(const void* ptr) {
   hipPointerAttribute_t a;
   const hipError_t e = hipPointerGetAttributes(&a, ptr);
@@ -147,7 +162,7 @@ static int host_pipeline(const Problem& p, bool encode, void* h_data, void* h_st
   const size_t data_bytes = total_vals * es;
   const size_t sbytes = stream_bytes_of(g);
   const size_t wave_bytes = (size_t)g.maxbits * 8;  // stream bytes per full wave
-  const size_t per = std::max<size_t>(1, kChunkBytes / (slab_vals * es));
+  const size_t per = std::max<size_t>(1, chunk_bytes() / (slab_vals * es));
 
   std::vector<Chunk> chunks;
   uint32_t w_prev = 0;

@@ -32,7 +32,10 @@ bool is_device_ptr(const void* p) {
   return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
 }
 
+thread_local int t_last_status = CUZFP_SUCCESS;
+
 void report(const char* what, int rc) {
+  t_last_status = rc;
   std::fprintf(stderr, "cuZFP: %s failed: %s", what, cuzfp_hip_status_string(rc));
   if (rc == CUZFP_ERROR_HIP)
     std::fprintf(stderr, " (%s)", hipGetErrorString((hipError_t)cuzfp_hip_last_hip_error()));
@@ -88,6 +91,7 @@ int stage_field(zfp_field* f, bool upload, DeviceField* df) {
 }  // namespace
 
 size_t compress(zfp_stream* stream, zfp_field* field) {
+  t_last_status = CUZFP_SUCCESS;
   if (!stream || !field || !stream->stream || !field->data) {
     report("compress", CUZFP_ERROR_INVALID_ARGUMENT);
     return 0;
@@ -133,6 +137,7 @@ size_t compress(zfp_stream* stream, zfp_field* field) {
 }
 
 void decompress(zfp_stream* stream, zfp_field* field) {
+  t_last_status = CUZFP_SUCCESS;
   if (!stream || !field || !stream->stream || !field->data) {
     report("decompress", CUZFP_ERROR_INVALID_ARGUMENT);
     return;
@@ -175,3 +180,6 @@ void decompress(zfp_stream* stream, zfp_field* field) {
 }
 
 }  // namespace cuZFP
+
+// extension: the status of this thread's last compress / decompress call
+extern "C" int cuZFP_last_status(void) { return cuZFP::t_last_status; }

@@ -196,6 +196,24 @@ struct LdsReader {
     e2a = ((lds_u32*)(uintptr_t)a2)[0];
     e2b = ((lds_u32*)(uintptr_t)a2)[1u << kChunkBits];
   }
+  // continuation pairs (dense planes): 32 stream bits at bit q of the block,
+  // chunk A in state st (0/1), chunk B in states 0 and 1
+  __device__ __forceinline__ uint32_t window32(uint32_t q) const {
+    lds_u32* t = row(q);
+    return __builtin_amdgcn_alignbit(t[64], t[0], q);
+  }
+  __device__ __forceinline__ void chunks_st(uint32_t g, uint32_t st, uint32_t& eA, uint32_t& eBa,
+                                            uint32_t& eBb) const {
+    const uint32_t base = (uint32_t)(uintptr_t)(lds_u32*)lut32;
+    const uint32_t cA = (g & kChunkMask) | (st << kChunkBits);
+    uint32_t aA, c2, a2;
+    asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(aA) : "v"(cA), "s"(base));
+    asm("v_bfe_u32 %0, %1, %2, %2" : "=v"(c2) : "v"(g), "i"(kChunkBits));
+    asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a2) : "v"(c2), "s"(base));
+    eA = ((lds_u32*)(uintptr_t)aA)[0];
+    eBa = ((lds_u32*)(uintptr_t)a2)[0];
+    eBb = ((lds_u32*)(uintptr_t)a2)[1u << kChunkBits];
+  }
   __device__ __forceinline__ uint32_t chunk1(uint32_t g, bool group) const {
     const uint32_t base = (uint32_t)(uintptr_t)(lds_u32*)lut32;
     const uint32_t c1 = group ? (g & kChunkMask) : kNoGroupEntry - (2u << kChunkBits);
@@ -247,6 +265,7 @@ struct RegReader : LdsReader<PRIO> {
     g = (uint32_t)at(this->pos + m);
   }
   __device__ __forceinline__ uint64_t peek() const { return at(this->pos); }
+  __device__ __forceinline__ uint32_t window32(uint32_t q) const { return (uint32_t)at(q); }
   __device__ __forceinline__ void peek2(uint64_t& a, uint64_t& b) const {
     a = at(this->pos);
     b = 0;  // bits past 64: past the block

@@ -1120,6 +1120,17 @@ ZFP_HD uint32_t keep_if_bit13(uint32_t v, uint32_t e) {
 // gated on `slow`: a lane out of budget (b1 = 0) reads zeros past its block
 // (its group test reads as a "0" it does not consume), and a plane with no
 // group part (n = N) looks up the empty entry.
+// v unless bit 13 of e is set (v_bfe_i32 + v_bfi_b32)
+ZFP_HD uint32_t drop_if_bit13(uint32_t v, uint32_t e) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t m;
+  asm("v_bfe_i32 %0, %1, 13, 1" : "=v"(m) : "v"(e));
+  return v & ~m;
+#else
+  return (e >> 13) & 1u ? 0u : v;
+#endif
+}
+
 template <int DIMS, typename PW, typename Reader>
 ZFP_HD PW decode_plane_lut(unsigned& bits, unsigned& n, Reader& rd, bool& slow) {
   constexpr unsigned N = 1u << (2 * DIMS);
@@ -1152,14 +1163,110 @@ ZFP_HD PW decode_plane_lut(unsigned& bits, unsigned& n, Reader& rd, bool& slow) 
   // host reader guarantee it) and the budget always ends there, so a code
   // whose last one is the budget's last bit ends here one bit past the budget
   // (its zero group test is not in the stream): the reference keeps that one
-  // and reads no more (decode.c:302-317).  Any other code the budget cuts
-  // short takes the general decoder.  (N - 1 - n is huge for n = N.)
+  // and reads no more (decode.c:302-317).  Codes longer than the two chunks
+  // and codes the budget cuts short take decode_plane_cont; a code reaching
+  // position N-1 the general decoder.  (N - 1 - n is huge for n = N.)
   slow = !(used <= b1 + 1 && npos <= N - 1 - n);
   // the verbatim bits below m, the new ones at n >= m: one v_bfi_b32 a dword
   const PW o = (PW)ones << (n & (8 * sizeof(PW) - 1));
   const PW x = ((PW)vmask & (PW)w) | (~(PW)vmask & o);
   n += npos;
   const unsigned adv = m + umin(used, b1);
+  rd.pos += adv;
+  bits -= adv;
+  return x;
+}
+
+// The table step for the planes decode_plane_lut leaves (a dense plane's
+// code longer than two chunks, or a code the budget cuts short): the same
+// first chunk pair, further pairs while the budget reaches past what has been
+// read, and the budget cut resolved from the table sums.  Sets `slow` for what
+// is left (a code reaching position N-1, where the one is implied) to the
+// general decoder.
+template <int DIMS, typename PW, typename Reader>
+ZFP_HD PW decode_plane_cont(unsigned& bits, unsigned& n, Reader& rd, bool& slow) {
+  constexpr unsigned N = 1u << (2 * DIMS);
+  const unsigned m = umin(n, bits);
+  uint64_t w;
+  uint32_t g;
+  rd.windows(m, w, g);
+  const uint64_t vmask = lowmask64(m);
+  const unsigned b1 = bits - m;                // budget after the verbatim bits
+  // chunk 1 starts at the leading group test (table state 2), chunk 2 is read
+  // in both states and chosen by chunk 1's exit state; nothing follows a
+  // chunk 1 that ended the code
+  uint32_t e1, e2;
+  if constexpr (DIMS == 1) {
+    // a 1D code (4 positions, at most 7 bits with the leading test) fits chunk 1
+    e1 = rd.chunk1(g, n < N);
+    e2 = 0;
+  } else {
+    uint32_t e2a, e2b;
+    rd.chunks(g, n < N, e1, e2a, e2b);
+    const uint32_t e2s = (e1 & kEntryState) ? e2b : e2a;
+    e2 = keep_if_bit13(e2s, e1);  // nothing after a chunk 1 that ended
+  }
+  const uint32_t S = e1 + e2;                  // field-wise sums
+  uint32_t npos = S >> kPosShift & 31u;
+  const uint32_t used0 = S & kUsedMask;        // >= kNotEnded: the code has not ended
+  bool ended = used0 < kNotEnded;
+  uint32_t parsed = ended ? used0 : used0 - kNotEnded;  // code bits read (all of them if not ended)
+  uint64_t ones = ((e1 >> kOnesShift) & kChunkMask) |
+                  (((e2 >> kOnesShift) & kChunkMask) << ((e1 >> kPosShift) & 31u));
+  uint32_t st = (DIMS == 1 ? e1 : e2) >> 31;  // exit state of the last chunk read (code not ended)
+  if constexpr (DIMS >= 2) {
+    // A code longer than the two chunks (a dense plane, the last few of a
+    // block): further chunk pairs from the exit state, while the budget
+    // reaches past what has been read.  In a continuation pair both chunks
+    // are in state 0/1, whose entries carry the marker when they end.
+    bool open = !ended && parsed < b1 && n + npos < N;
+    if (__builtin_expect(any_lane(open), 0)) {
+      while (any_lane(open)) {
+        if (open) {
+          const uint32_t gg = rd.window32(rd.pos + m + parsed);
+          uint32_t eA, eBa, eBb;
+          rd.chunks_st(gg, st, eA, eBa, eBb);
+          const uint32_t eB = drop_if_bit13((eA & kEntryState) ? eBb : eBa, eA);
+          const uint32_t T = eA + eB;
+          const uint32_t pA = (eA >> kPosShift) & 31u;
+          const uint64_t o = ((eA >> kOnesShift) & kChunkMask) | (((eB >> kOnesShift) & kChunkMask) << pA);
+          ones |= o << (npos & 63u);
+          npos += (T >> kPosShift) & 31u;
+          const uint32_t u = T & kUsedMask;
+          ended = u >= kNotEnded;
+          parsed += u & (kNotEnded - 1u);
+          st = eB >> 31;
+          open = !ended && parsed < b1 && n + npos < N;
+        }
+      }
+    }
+  }
+  // The stream reads as zeros past the block's last bit (the kernels and the
+  // host reader guarantee it) and the budget always ends there.  So:
+  //  - a code that ended within the budget, or one bit past it (a one read
+  //    with the budget's last bit, followed by the zero group test that is
+  //    not in the stream), is taken as read;
+  //  - a code the budget cut short at a token boundary reads on as zero
+  //    positions: the reference deposited one more one at the position it
+  //    had reached when the budget ran out (decode.c:305-311), and that
+  //    position is npos less the bits read past the budget.
+  // Positions must stay below N-1 (there the one is implied and not read);
+  // anything else takes the general decoder.  (N - 1 - n is huge for n = N.)
+  // (a code read up to the budget's last bit that ends there with a one --
+  // exit state 1, its group test past the block -- ended as read)
+  if (!ended && parsed == b1 && st) {
+    ended = true;
+    parsed = b1 + 1u;
+  }
+  const bool cut = !ended && parsed >= b1;
+  const uint32_t P = cut ? npos - (parsed - b1) : npos;
+  slow = cut ? !(P <= N - 1 - n) : !(ended && parsed <= b1 + 1 && npos <= N - 1 - n);
+  ones |= (uint64_t)(cut ? 1u : 0u) << (P & 63u);
+  // the verbatim bits below m, the new ones at n >= m: one v_bfi_b32 a dword
+  const PW o = (PW)ones << (n & (8 * sizeof(PW) - 1));
+  const PW x = ((PW)vmask & (PW)w) | (~(PW)vmask & o);
+  n += cut ? P + 1u : npos;
+  const unsigned adv = m + (cut ? b1 : umin(parsed, b1));
   rd.pos += adv;
   bits -= adv;
   return x;
@@ -1178,7 +1285,15 @@ ZFP_HD PW decode_plane_any(unsigned& bits, unsigned& n, Reader& rd) {
       rd.init(pos0);
       n = n0;
       bits = bits0;
-      x = decode_plane<DIMS, PW>(bits, n, rd);
+      x = decode_plane_cont<DIMS, PW>(bits, n, rd, slow);
+    }
+    if (__builtin_expect(any_lane(slow), 0)) {
+      if (slow) {
+        rd.init(pos0);
+        n = n0;
+        bits = bits0;
+        x = decode_plane<DIMS, PW>(bits, n, rd);
+      }
     }
   }
   return x;

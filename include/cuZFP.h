@@ -11,9 +11,13 @@
 //   - compress returns the compressed byte count (ceil(blocks*maxbits/64)*8).
 // Differences, all in the direction of CPU zfp 0.5.0 (the reference's own
 // oracle, src/utils/test.py:68-93): non-zero field strides are honoured; any
-// maxbits >= 1 + exponent bits works in every dimensionality; partial blocks
-// are padded as CPU zfp pads them; failures print one line to stderr and
-// compress returns 0 (the reference prints and continues).
+// maxbits in [1 + exponent bits, CUZFP_MAX_BITS = 6144] works in every
+// dimensionality (zfp's ZFP_MAX_BITS, the most bits a block can use, is 4171);
+// partial blocks are padded as CPU zfp pads them; failures print one line to
+// stderr and compress returns 0 (the reference prints and continues).
+// One addition: cuZFP_last_status() returns the status code (include/cuzfp_hip.h)
+// of the calling thread's last compress / decompress, 0 on success, so a caller
+// of the void decompress can tell that it failed.
 #ifndef cuZFP_h
 #define cuZFP_h
 
@@ -27,5 +31,7 @@ size_t compress(zfp_stream* stream, zfp_field* field);
 void decompress(zfp_stream* stream, zfp_field* field);
 
 }  // namespace cuZFP
+
+extern "C" int cuZFP_last_status(void);
 
 #endif

@@ -56,6 +56,13 @@ extern "C" {
 #define CUZFP_TYPE_FLOAT 3
 #define CUZFP_TYPE_DOUBLE 4
 
+/* Largest accepted maxbits (bits per block).  Calls with more return
+ * CUZFP_ERROR_INVALID_ARGUMENT.  It is above ZFP_MAX_BITS = 4171
+ * (zfp_structs.h:12), the most bits any block can use; beyond that a stream is
+ * padding.  The bound keeps one wave's LDS stream image within a workgroup's
+ * 64 KiB. */
+#define CUZFP_MAX_BITS 6144
+
 typedef enum {
   CUZFP_SUCCESS = 0,
   CUZFP_ERROR_INVALID_ARGUMENT = 1, /* bad dims, maxbits or null pointer   */

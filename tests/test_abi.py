@@ -104,3 +104,48 @@ def test_argument_errors(libs):
     assert lib.cuzfp_hip_compress_host(None, 3, 16, 16, 16, 512, buf, 1 << 20, ctypes.byref(got), 2) == 1
     with pytest.raises(cz.CodecError):
         cz.stream_bytes((16, 16, 16), np.float32, 3)
+
+
+def test_maxbits_cap(libs):
+    """maxbits up to CUZFP_MAX_BITS (6144, above zfp's ZFP_MAX_BITS = 4171) is
+    accepted; above it every entry point rejects the call (the decoder's LDS
+    stream image would no longer fit a workgroup)."""
+    lib = cz.library()
+    cap = int(re.search(r"#define CUZFP_MAX_BITS (\d+)", open(HEADER).read()).group(1))
+    assert cap == 6144
+    assert cz.stream_bytes((16, 16, 16), np.float64, cap) == 64 * cap // 8
+    with pytest.raises(cz.CodecError):
+        cz.stream_bytes((16, 16, 16), np.float64, cap + 1)
+    got = ctypes.c_size_t(0)
+    buf = ctypes.c_void_p(0x1000)  # never dereferenced: rejected before any launch
+    assert lib.cuzfp_hip_encode(buf, 4, 16, 16, 16, 0, 0, 0, cap + 1, buf, 1 << 30, ctypes.byref(got), None) == 1
+    assert lib.cuzfp_hip_decode(buf, 1 << 30, 4, 16, 16, 16, 0, 0, 0, cap + 1, buf, None) == 1
+    assert lib.cuzfp_hip_maximum_size(3, 16, 16, 16, cap + 1) == 0
+
+
+def test_host_out_checks(libs):
+    """compress_host / decompress_host validate a caller's `out` before the
+    C side writes through it (contiguity, dtype, shape, size)."""
+    a = np.zeros((8, 8, 8), np.float32)
+    mb = 512
+    need = cz.stream_bytes(a.shape, a.dtype, mb)
+    with pytest.raises(ValueError):
+        cz.compress_host(a, mb, out=np.empty(need // 8 - 1, np.uint64))
+    with pytest.raises(ValueError):
+        cz.compress_host(a, mb, out=np.empty(2 * (need // 8), np.uint64)[::2])
+    words = np.zeros(need // 8, np.uint64)
+    with pytest.raises(ValueError):
+        cz.decompress_host(words, a.shape, np.float32, mb, out=np.empty((8, 8, 8), np.float64))
+    with pytest.raises(ValueError):
+        cz.decompress_host(words, a.shape, np.float32, mb, out=np.empty((8, 8, 16), np.float32)[:, :, ::2])
+    with pytest.raises(ValueError):
+        cz.decompress_host(words, a.shape, np.float32, mb, out=np.empty((8, 8, 4), np.float32))
+
+
+def test_broadcast_views_detected():
+    torch = pytest.importorskip("torch")
+    assert cz._broadcast(torch.zeros(4).expand(8, 4))
+    assert cz._broadcast(torch.zeros(1, 4).expand(3, 4))
+    assert not cz._broadcast(torch.zeros(8, 4))
+    assert not cz._broadcast(torch.zeros(1, 4))  # stride is irrelevant on an axis of extent 1
+    assert not cz._broadcast(torch.zeros(8, 8)[:, ::2])

@@ -359,3 +359,58 @@ def test_register_reader(cuda, restatement, dims, dtype):
             ref = restatement.compress(a, mb)
             assert np.array_equal(w, ref), mb
             assert np.array_equal(y.view(np.uint8), restatement.decompress(ref, shape, dtype, mb).view(np.uint8)), mb
+
+
+@pytest.mark.parametrize("shape,dtype,rate", [((64, 48, 40), np.float32, 8), ((24, 20, 16), np.float64, 16),
+                                              ((300, 260), np.float32, 4), ((200003,), np.float32, 8)])
+@pytest.mark.parametrize("pinned", [False, True])
+def test_host_pipeline_multi_chunk(cuda, restatement, monkeypatch, shape, dtype, rate, pinned):
+    """The host pipeline with chunks far smaller than the array
+    (CUZFP_HOST_CHUNK_BYTES): waves straddling chunks, the cross-stream event
+    waits and the pageable staging ring, for 1, 2 and 3 streams."""
+    import torch
+    from cuzfp_amd.datagen import splitmix_uniform
+    a = splitmix_uniform(shape, dtype, seed=9)
+    mb = cz.rate_to_maxbits(rate, dtype, len(shape))
+    ref = restatement.compress(a, mb)
+    want = restatement.decompress(ref, shape, dtype, mb)
+    out = None
+    if pinned:
+        a = torch.from_numpy(a).pin_memory().numpy()
+        out = torch.empty(cz.stream_bytes(shape, dtype, mb) // 8, dtype=torch.int64).pin_memory().numpy().view(np.uint64)
+    slab = a.nbytes // (shape[0] // 4 if len(shape) > 1 else max(1, shape[0] // 4))
+    for chunk in (1, 3 * slab + 5, a.nbytes // 7):
+        monkeypatch.setenv("CUZFP_HOST_CHUNK_BYTES", str(chunk))
+        for nstreams in (1, 2, 3):
+            s = cz.compress_host(a, mb, nstreams=nstreams, out=out)
+            assert np.array_equal(s, ref), (chunk, nstreams)
+            y = cz.decompress_host(s, shape, dtype, mb, nstreams=nstreams)
+            assert np.array_equal(y, want), (chunk, nstreams)
+
+
+def test_broadcast_view_encodes_materialised(cuda, restatement):
+    """An expanded tensor (a zero stride) encodes as its materialised copy;
+    decoding into a broadcast view is refused."""
+    import torch
+    base = torch.linspace(-1, 1, 16, dtype=torch.float32, device=cuda)
+    x = base.expand(12, 16)
+    mb = cz.rate_to_maxbits(8, np.float32, 2)
+    w = cz.encode(x, mb)
+    ref = restatement.compress(np.ascontiguousarray(x.cpu().numpy()), mb)
+    assert np.array_equal(w.cpu().numpy().view(np.uint64), ref)
+    with pytest.raises(ValueError):
+        cz.decode(w, (12, 16), torch.float32, mb, out=torch.empty(16, dtype=torch.float32, device=cuda).expand(12, 16))
+
+
+@pytest.mark.parametrize("dims,dtype", [(3, np.float64), (3, np.float32), (2, np.float64), (1, np.float32)])
+def test_largest_maxbits(cuda, restatement, dims, dtype):
+    """maxbits at the cap (CUZFP_MAX_BITS = 6144): the widest LDS stream images
+    (one wave per workgroup) against the oracle."""
+    from cuzfp_amd.datagen import splitmix_uniform
+    shape = {1: (1000,), 2: (36, 28), 3: (12, 8, 20)}[dims]
+    a = splitmix_uniform(shape, dtype, seed=3)
+    for mb in (6144, 6143, 4171):
+        words, y = _gpu_roundtrip(a, mb, cuda)
+        ref = restatement.compress(a, mb)
+        assert np.array_equal(words, ref), mb
+        assert np.array_equal(y, restatement.decompress(ref, shape, dtype, mb)), mb

@@ -31,6 +31,14 @@ struct Rd {
   uint32_t chunk1(uint32_t g, bool group) const {
     return table().e[group ? (2u << cuzfp::kChunkBits) | (g & cuzfp::kChunkMask) : cuzfp::kNoGroupEntry];
   }
+  uint32_t window32(size_t q) { const size_t p = pos; pos = q; const uint32_t v = (uint32_t)peek(); pos = p; return v; }
+  void chunks_st(uint32_t g, uint32_t st, uint32_t& eA, uint32_t& eBa, uint32_t& eBb) const {
+    const uint32_t* t = table().e;
+    const uint32_t c2 = (g >> cuzfp::kChunkBits) & cuzfp::kChunkMask;
+    eA = t[(st << cuzfp::kChunkBits) | (g & cuzfp::kChunkMask)];
+    eBa = t[c2];
+    eBb = t[c2 + (1u << cuzfp::kChunkBits)];
+  }
 };
 struct Wr {
   uint64_t* s; size_t pos, end;
