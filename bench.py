@@ -17,7 +17,18 @@ Prints one JSON line on rank 0 (the driver contract), with
   value       = input GB/s of all ranks (10^9 B of input / s)
   roofline    = the dominant kernel's algorithmic bytes / its mean duration,
                 over the MI355X HBM3E peak (8.0 TB/s, MI355X_MICROARCH.md)
-  cpu_baseline= the reference's own CPU zfp 0.5.0 (oracle/_ref), timed here.
+  cpu_baseline= the reference's own CPU zfp 0.5.0 (oracle/_ref), timed here
+                on this GPU's share of the host cores, for the headline array
+                and for BASELINE configs[0] (1D f32 1M sine field, rate 8)
+  config5     = BASELINE configs[4] at this N: one 1024^3 f32 array at rate 8
+                strong-scaled over the N ranks as z-slabs of 1024/N planes,
+                its step time (max over ranks), per-rank kernel times, the RCCL
+                all-gather of the compressed stream and the gathered stream's
+                SHA-256 against the reference's (tests/golden/golden.json)
+  hbm_copy    = achievable bandwidth: cuzfp_hip_copy (16-byte non-temporal
+                copy kernel) and torch's copy_, at 1 GiB and at the input size
+  host_path   = the pinned host pipeline's rates and the bare pinned H2D/D2H
+                link rates measured in the same run.
 """
 from __future__ import annotations
 
@@ -58,17 +69,32 @@ def parse():
     p.add_argument("--no-host-path", action="store_true")
     p.add_argument("--no-copy-probe", action="store_true", help="skip the device-to-device copy bandwidth probe")
     p.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
+    p.add_argument("--no-config5", action="store_true", help="skip BASELINE configs[4] (1024^3 sharded)")
+    p.add_argument("--config5-edge", type=int, default=1024, help="edge of configs[4]'s global array")
+    p.add_argument("--config5-steps", type=int, default=10)
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     return p.parse_args()
 
 
+def cpu_share() -> tuple[int, int]:
+    """(threads used, CPUs in this process's affinity).  On the GPU box one
+    GPU's share of the host is OMP_NUM_THREADS (16): the harness sizes every
+    CPU pool to it, and so does the baseline."""
+    aff = len(os.sched_getaffinity(0))
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or aff
+    return max(1, min(aff, share)), aff
+
+
 def cpu_baseline(a: np.ndarray, maxbits: int):
     """Reference CPU zfp 0.5.0 (zfp_compress + zfp_decompress, oracle/_ref) on
-    this process's host cores: the whole workload array, slab-parallel over up
-    to 16 threads, median of 30 round trips (about 10-15 core-seconds); plus one
-    core on the first quarter of the array."""
+    this process's host cores: the whole headline array, slab-parallel over
+    this GPU's share of the cores, median of 30 round trips (10-15 core-s);
+    one core on a quarter of it; and BASELINE configs[0], the reference's own
+    CPU test (src/tests/t_encode_decode_1.cpp:15-30: 1M float32 sine values,
+    rate 8), median of 30 single-core round trips."""
     try:
         import oracle
+        from cuzfp_amd.datagen import sine_field
     except Exception:  # pragma: no cover
         return None
     ref = oracle.reference
@@ -77,11 +103,14 @@ def cpu_baseline(a: np.ndarray, maxbits: int):
         return None
     sample = np.ascontiguousarray(a)
     quarter = np.ascontiguousarray(a[: max(4, (a.shape[0] // 16) * 4)])
-    cores = max(1, min(16, len(os.sched_getaffinity(0))))
+    cores, aff = cpu_share()
     reps = 30
     t0 = time.perf_counter()
     rt, enc, dec, _ = ref.time_roundtrip(sample, maxbits, threads=cores, reps=reps)
     rt1, enc1, dec1, _ = ref.time_roundtrip(quarter, maxbits, threads=1, reps=3)
+    s1 = sine_field(1 << 20, np.float32)
+    mb1 = int(oracle.restatement.rate_to_maxbits(8, np.float32, 1)) if oracle.restatement else 32
+    rtc0, encc0, decc0, _ = ref.time_roundtrip(s1, mb1, threads=1, reps=reps)
     wall = time.perf_counter() - t0
     nbytes = sample.nbytes
     model = None
@@ -90,12 +119,137 @@ def cpu_baseline(a: np.ndarray, maxbits: int):
     except Exception:  # pragma: no cover
         pass
     return {"value": round(nbytes / rt / 1e9, 4), "unit": "GB/s", "cores": cores, "kind": kind,
-            "cpu_model": model, "host_cpus_visible": os.cpu_count(),
+            "cpu_model": model, "host_cpus_visible": os.cpu_count(), "cpu_affinity": aff,
+            "cores_note": "threads = this GPU's share of the host (OMP_NUM_THREADS on the GPU box, which "
+                          "sizes every CPU pool to it); the whole machine's CPUs serve 8 GPUs",
             "sample": f"the whole {'x'.join(map(str, sample.shape))} {sample.dtype} workload array, maxbits "
                       f"{maxbits}, median of {reps} round trips, slab threads (slowest axis)",
             "encode_GBps": round(nbytes / enc / 1e9, 4), "decode_GBps": round(nbytes / dec / 1e9, 4),
             "single_core_GBps": round(quarter.nbytes / rt1 / 1e9, 4),
+            "config0": {"workload": "1d_float32_1M_rate8 (t_encode_decode_1.cpp sine field)", "cores": 1,
+                        "roundtrip_GBps": round(s1.nbytes / rtc0 / 1e9, 4),
+                        "encode_GBps": round(s1.nbytes / encc0 / 1e9, 4),
+                        "decode_GBps": round(s1.nbytes / decc0 / 1e9, 4),
+                        "roundtrip_ms": round(rtc0 * 1e3, 3), "maxbits": mb1,
+                        "sample": f"median of {reps} single-core round trips"},
             "wall_s": round(wall, 2)}
+
+
+def run_config5(E: int, steps: int, world: int, rank: int, dev, graphed, dist):
+    """BASELINE configs[4] at this N: one E^3 f32 polynomial array at
+    rate 8 strong-scaled over the N ranks as z-slabs of E/N planes.  Each rank
+    encodes and decodes its slab (no communication); the step time is the max
+    over ranks of K steps between barriers.  Then, outside the timed region,
+    the RCCL all-gather that assembles the global stream on every rank, timed
+    with HIP events on the launch stream; and parity: every rank's segment and
+    the gathered stream against the reference's SHA-256s, the round-trip error
+    against the reference's."""
+    import torch
+    import cuzfp_amd as cz
+    from cuzfp_amd import dist as zd
+    stream = torch.cuda.current_stream()
+    maxbits = cz.rate_to_maxbits(8, np.float32, 3)
+    sh = zd.StrongShard(E, world, rank, maxbits)
+    from cuzfp_amd.datagen import polynomial_slab_device
+    x = polynomial_slab_device(sh.global_shape, sh.z0, sh.z1, dev)
+    words = torch.empty(sh.words, dtype=torch.int64, device=dev)
+    y = torch.empty_like(x)
+
+    def step():
+        cz.encode(x, maxbits, out=words)
+        cz.decode(words, sh.shape, x.dtype, maxbits, out=y)
+
+    step()
+    torch.cuda.synchronize()
+    max_err = float((y - x).abs().max().item())
+
+    def allmax(v: float) -> float:
+        t = torch.tensor([v], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def allgather_floats(v: float) -> list:
+        t = torch.tensor([v], dtype=torch.float64, device=dev)
+        if world == 1:
+            return [v]
+        out = torch.empty(world, dtype=torch.float64, device=dev)
+        dist.all_gather_into_tensor(out, t)
+        return [float(u) for u in out.cpu()]
+
+    per_graph = next(c for c in (5, 2, 1) if steps % c == 0)
+    run = graphed(step, per_graph)
+    run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps // per_graph):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    step_s = allmax((time.perf_counter() - t0) / steps)
+
+    def time_kernel(fn, reps=10):
+        r = graphed(fn, reps)
+        r()
+        torch.cuda.synchronize()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        r()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps * 1e-3
+
+    enc_s = allgather_floats(time_kernel(lambda: cz.encode(x, maxbits, out=words)))
+    dec_s = allgather_floats(time_kernel(lambda: cz.decode(words, sh.shape, x.dtype, maxbits, out=y)))
+    cz.encode(x, maxbits, out=words)
+    torch.cuda.synchronize()
+
+    gold = None
+    gpath = os.path.join(ROOT, "tests", "golden", "golden.json")
+    if os.path.exists(gpath):
+        gold = json.load(open(gpath))["cases"].get(f"baseline/3d_f32_{E}_r8/polynomial")
+    local = words.cpu().numpy()
+    slab_ok = None
+    if gold and world > 1 and f"slab_sha256_n{world}" in gold:
+        slab_ok = hashlib.sha256(local.tobytes()).hexdigest() == gold[f"slab_sha256_n{world}"][rank]
+        slab_ok = allmax(0.0 if slab_ok else 1.0) == 0.0
+
+    ag_s = None
+    if world > 1:
+        full = zd.allgather_stream(words)
+        torch.cuda.synchronize()
+        dist.barrier()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(5):
+            full = zd.allgather_stream(words)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        dist.barrier()
+        ag_s = allmax(e0.elapsed_time(e1) / 5 * 1e-3)
+        full_host = full.cpu().numpy() if rank == 0 else None
+        del full
+    else:
+        full_host = local
+    out = zd.sharded_summary(sh, 4, step_s, enc_s, dec_s, HBM_PEAK_GBS, ag_s)
+    out["steps"] = steps
+    out["max_abs_err"] = allmax(max_err)
+    if rank == 0:
+        got = hashlib.sha256(full_host.tobytes()).hexdigest()
+        out["parity"] = {"reference_sha256": gold["stream_sha256"] if gold else None,
+                         "gathered_stream_sha256": got,
+                         "stream_matches_reference": (got == gold["stream_sha256"]) if gold else None,
+                         "slabs_match_reference_word_ranges": slab_ok,
+                         "max_abs_err_matches_reference": (out["max_abs_err"] == gold["max_abs_err"]) if gold else None}
+    del x, y, words
+    torch.cuda.empty_cache()
+    return out
 
 
 def main():
@@ -226,12 +380,14 @@ def main():
     enc_ms = time_kernel(lambda: cz.encode(x, maxbits, out=words), reps)
     dec_ms = time_kernel(lambda: cz.decode(words, shape, x.dtype, maxbits, out=y), reps)
 
-    # achievable HBM bandwidth on this box: a device-to-device copy
-    # (torch's copy kernel, read + write) of the input's size and of 1 GiB
-    def copy_GBps(nbytes):
+    # achievable HBM bandwidth on this box: the library's 16-byte
+    # non-temporal copy kernel (cuzfp_hip_copy, the codec's access width and
+    # cache policy) and torch's copy_, read + write bytes over time
+    def copy_GBps(nbytes, fn_name):
         src = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
         dst = torch.empty_like(src)
-        r = graphed(lambda: dst.copy_(src), 10)
+        fn = (lambda: cz.copy(src, dst)) if fn_name == "cuzfp" else (lambda: dst.copy_(src))
+        r = graphed(fn, 10)
         r()
         torch.cuda.synchronize()
         e0 = torch.cuda.Event(enable_timing=True)
@@ -247,9 +403,11 @@ def main():
 
     hbm_copy = None
     if rank == 0 and not args.no_copy_probe:
-        hbm_copy = {"kernel": "torch copy_ (device to device)", "GBps_at_input_size": copy_GBps(a.nbytes),
-                    "GBps_1GiB": copy_GBps(1 << 30), "input_bytes": a.nbytes,
-                    "note": "read + write bytes / time, hipGraph of 10 copies"}
+        hbm_copy = {"kernel": "cuzfp_hip_copy (16-B non-temporal loads/stores, 4 in flight a lane)",
+                    "GBps_1GiB": copy_GBps(1 << 30, "cuzfp"), "GBps_at_input_size": copy_GBps(a.nbytes, "cuzfp"),
+                    "torch_copy_GBps_1GiB": copy_GBps(1 << 30, "torch"), "input_bytes": a.nbytes,
+                    "note": "read + write bytes / time, hipGraph of 10 copies; at the input size source and "
+                            "destination sit in the 256 MiB Infinity Cache between copies"}
 
     # optional RCCL all-gather of the compressed stream (the exchange step)
     allgather = None
@@ -270,6 +428,13 @@ def main():
                      "GBps_per_rank_in": round((full.numel() * 8 - nbytes_stream) / ag_s / 1e9, 2),
                      "backend": "nccl (RCCL)"}
         del full
+
+    config5 = None
+    if not args.no_config5 and dims == 3 and args.dtype == "float32" and not strong:
+        try:
+            config5 = run_config5(args.config5_edge, args.config5_steps, world, rank, dev, graphed, dist)
+        except torch.cuda.OutOfMemoryError as e:  # pragma: no cover
+            config5 = {"error": f"out of memory: {e}"}
 
     n_in = a.nbytes
     value = n_in * world * args.steps / elapsed / 1e9
@@ -308,9 +473,37 @@ def main():
             for _ in range(5):
                 cz.decompress_host(hp_out, shape, dtype, maxbits, out=hp_back)
             td = (time.perf_counter() - td) / 5
+            # the bare pinned link in the same run: H2D of the input's size, D2H of
+            # the stream's (the pipeline's two transfers), 5 each
+            h_in = torch.from_numpy(hp_in)
+            d_tmp = torch.empty(a.shape, dtype=x.dtype, device=dev)
+            h_s = torch.from_numpy(hp_out.view(np.int64))
+            torch.cuda.synchronize()
+            t_h2d = time.perf_counter()
+            for _ in range(5):
+                d_tmp.copy_(h_in, non_blocking=True)
+            torch.cuda.synchronize()
+            t_h2d = (time.perf_counter() - t_h2d) / 5
+            t_d2h = time.perf_counter()
+            for _ in range(5):
+                h_s.copy_(words, non_blocking=True)
+            torch.cuda.synchronize()
+            t_d2h = (time.perf_counter() - t_d2h) / 5
+            del d_tmp
+            h2d = n_in / t_h2d / 1e9
+            d2h = s_bytes / t_d2h / 1e9
+            # link-bound time of one compress = H2D of the input + D2H of the
+            # stream (decompress: the reverse); the pipeline overlaps them with
+            # the kernels, so its rate over this bound is its link efficiency
+            c_link = n_in / (n_in / (h2d * 1e9) + s_bytes / (d2h * 1e9)) / 1e9
             host_path = {"compress_GBps": round(n_in / tc / 1e9, 2), "decompress_GBps": round(n_in / td / 1e9, 2),
                          "roundtrip_GBps": round(n_in / (tc + td) / 1e9, 2),
-                         "note": "pinned host buffers, PCIe-inclusive (cuzfp_hip_compress_host/decompress_host)"}
+                         "link_GBps": {"h2d": round(h2d, 2), "d2h": round(d2h, 2)},
+                         "frac_of_link": {"compress": round(n_in / tc / 1e9 / c_link, 3),
+                                          "decompress": round(n_in / td / 1e9 / c_link, 3)},
+                         "chunk_bytes": int(os.environ.get("CUZFP_HOST_CHUNK_BYTES", 32 << 20)), "nstreams": 2,
+                         "note": "pinned host buffers, PCIe-inclusive (cuzfp_hip_compress_host/decompress_host); "
+                                 "frac_of_link = rate / (input bytes / (input/h2d + stream/d2h))"}
         cpu = None if (args.no_cpu_baseline or world > 1 or strong) else cpu_baseline(a, maxbits)
         result = {
             "metric": METRIC if (dims == 3 and args.dtype == "float32") else
@@ -343,6 +536,7 @@ def main():
             "cpu_baseline": cpu,
             "host_path": host_path,
             "allgather": allgather,
+            "config5": config5,
             "max_abs_err": max_err,
             "parity": parity,
         }

@@ -81,6 +81,8 @@ def library() -> ctypes.CDLL:
     lib.cuzfp_hip_compress_host.argtypes = [vp, i, u, u, u, u, vp, sz, ctypes.POINTER(sz), i]
     lib.cuzfp_hip_decompress_host.restype = i
     lib.cuzfp_hip_decompress_host.argtypes = [vp, sz, i, u, u, u, u, vp, i]
+    lib.cuzfp_hip_copy.restype = i
+    lib.cuzfp_hip_copy.argtypes = [vp, vp, sz, vp]
     _lib = lib
     return lib
 
@@ -202,6 +204,16 @@ def decode(words, shape, dtype, maxbits: int, out=None, stream=None):
                                     _stream_handle(stream))
     _check("decode", rc)
     return out
+
+
+def copy(src, dst, stream=None):
+    """Device-to-device copy through cuzfp_hip_copy (16-byte non-temporal
+    accesses): the bandwidth calibrator bench.py reports beside the codec."""
+    nbytes = src.numel() * src.element_size()
+    if dst.numel() * dst.element_size() < nbytes:
+        raise ValueError("copy: destination too small")
+    _check("copy", library().cuzfp_hip_copy(src.data_ptr(), dst.data_ptr(), nbytes, _stream_handle(stream)))
+    return dst
 
 
 def compress_host(a: np.ndarray, maxbits: int, nstreams: int = 2, out: np.ndarray | None = None):

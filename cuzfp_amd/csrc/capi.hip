@@ -284,6 +284,31 @@ static int host_pipeline(const Problem& p, bool encode, void* h_data, void* h_st
   return CUZFP_SUCCESS;
 }
 
+// ---------------------------------------------------------------------------
+// Bandwidth calibrator (cuzfp_hip_copy): a device-to-device copy with 16-byte
+// non-temporal loads and stores, four in flight per lane, the codec's own
+// access width and cache policy.  bench.py times it at 1 GiB beside the codec
+// as the achievable-HBM reference (roofline.frac_of_copy).
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void copy16_nt(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                 size_t n16) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    const u32x4 a = __builtin_nontemporal_load(src + i);
+    const u32x4 b = __builtin_nontemporal_load(src + i + stride);
+    const u32x4 c = __builtin_nontemporal_load(src + i + 2 * stride);
+    const u32x4 d = __builtin_nontemporal_load(src + i + 3 * stride);
+    __builtin_nontemporal_store(a, dst + i);
+    __builtin_nontemporal_store(b, dst + i + stride);
+    __builtin_nontemporal_store(c, dst + i + 2 * stride);
+    __builtin_nontemporal_store(d, dst + i + 3 * stride);
+  }
+  for (; i < n16; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+}
+
 }  // namespace cuzfp
 
 
@@ -357,6 +382,23 @@ int cuzfp_hip_decode(const uint64_t* d_stream, size_t stream_bytes, int type, un
   if (!d_data || !d_stream) return CUZFP_ERROR_INVALID_ARGUMENT;
   if (stream_bytes < stream_bytes_of(p.g)) return CUZFP_ERROR_BUFFER_TOO_SMALL;
   return launch_decode(p, d_stream, d_data, 0, waves_of(p.g), stream);
+}
+
+int cuzfp_hip_copy(const void* d_src, void* d_dst, size_t bytes, hipStream_t stream) {
+  if (!d_src || !d_dst || (bytes & 15) || (((uintptr_t)d_src | (uintptr_t)d_dst) & 15))
+    return CUZFP_ERROR_INVALID_ARGUMENT;
+  if (!bytes) return CUZFP_SUCCESS;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  const size_t n16 = bytes / 16;
+  const size_t want = (n16 + 255) / 256;
+  const unsigned grid = (unsigned)std::min<size_t>(want, (size_t)cus * 8);
+  hipLaunchKernelGGL(copy16_nt, dim3(grid), dim3(256), 0, stream, (const u32x4*)d_src, (u32x4*)d_dst, n16);
+  const hipError_t e = hipGetLastError();
+  t_last_hip = e;
+  return e == hipSuccess ? CUZFP_SUCCESS : CUZFP_ERROR_HIP;
 }
 
 int cuzfp_hip_compress_host(const void* h_data, int type, unsigned nx, unsigned ny,

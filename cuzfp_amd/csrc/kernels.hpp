@@ -83,6 +83,9 @@ struct LdsOrWriter {
   uint64_t* p;          // the lane's column: word j at p[64 j], W + kSlackWords words, zeroed
   const uint32_t* lut;  // the workgroup's spread table
   uint32_t pos, lim;    // bits produced; 64 * W
+#if defined(CUZFP_EXP_NOPUT)
+  uint64_t sink = 0;
+#endif
   __device__ __forceinline__ bool full() const { return pos >= lim; }
   __device__ __forceinline__ void put(uint64_t v, unsigned n) {  // v < 2^n
     const uint32_t w = pos >> 6, sh = pos & 63;
@@ -93,7 +96,11 @@ struct LdsOrWriter {
   }
   __device__ __forceinline__ uint32_t spread(uint32_t b) const { return lut[b]; }
   __device__ __forceinline__ void zero_bit() { pos++; }
+#if defined(CUZFP_EXP_NOPUT)
+  __device__ __forceinline__ void finish() { p[0] ^= sink; }
+#else
   __device__ __forceinline__ void finish() {}
+#endif
   // a full lane keeps stepping with its wave: restart it at the first slack
   // row each plane, so its (discarded) pieces stay within rows W .. W + 3
   __device__ __forceinline__ void settle() { pos = pos < lim ? pos : lim; }
@@ -109,6 +116,9 @@ struct LdsBitWriter {
   const uint32_t* lut;     // the workgroup's spread table
   uint32_t pos, end, cnt;  // pos: stream offset of acc's bit 0
   uint64_t acc;
+#if defined(CUZFP_EXP_NOPUT)
+  uint64_t sink = 0;
+#endif
   __device__ __forceinline__ uint32_t spread(uint32_t b) const { return lut[b]; }
   __device__ __forceinline__ bool full() const { return pos + cnt >= end; }
   __device__ __forceinline__ void emit(uint64_t v) {
@@ -172,6 +182,11 @@ struct LdsReader {
   }
   // table decoder: 64 bits at pos and 32 bits at pos + m, read fresh
   __device__ __forceinline__ void windows(uint32_t m, uint64_t& w, uint32_t& g) const {
+#if defined(CUZFP_EXP_DEC_NOWIN)  // timing experiment (tools/variants.py): no window reads, wrong output
+    w = (uint64_t)(pos * 0x9e3779b9u) * 0x100000001ull;
+    g = (pos + m) * 0x85ebca6bu;
+    return;
+#endif
     const uint32_t q = pos + m;
     lds_u32* r = row(pos);
     lds_u32* t = row(q);
@@ -186,6 +201,12 @@ struct LdsReader {
   // (the compiler's forms take three)
   __device__ __forceinline__ void chunks(uint32_t g, bool group, uint32_t& e1, uint32_t& e2a,
                                          uint32_t& e2b) const {
+#if defined(CUZFP_EXP_DEC_NOLUT)  // timing experiment: no table reads (short ended codes), wrong output
+    e1 = pack_entry(g & 0x3ffu, ((g >> 10) & 7u) + 1u, ((g >> 13) & 7u) + 1u, 0);
+    e2a = e2b = 0;
+    (void)group;
+    return;
+#endif
     const uint32_t base = (uint32_t)(uintptr_t)(lds_u32*)lut32;
     const uint32_t c1 = group ? (g & kChunkMask) : kNoGroupEntry - (2u << kChunkBits);
     uint32_t a1, c2, a2;
@@ -432,14 +453,18 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 // Waves per SIMD the register budget is sized for: 4 (<= 128 VGPRs) in
-// general; 3D double blocks (64 x 64-bit values, 64 x 64-bit planes) need up
-// to 256 VGPRs, so 2, rather than spilling to scratch.
-template <typename Scalar, int DIMS> struct occupancy {
-  static constexpr int value = (sizeof(Scalar) == 8 && DIMS == 3) ? 2 : 4;
+// general.  3D double blocks hold 64 x 64-bit values (128 VGPRs) and then 64 x
+// 64-bit planes: the encoder fits 3 waves (<= 168 VGPRs), the decoder, whose
+// plane loop keeps more state live, 2 (<= 256) rather than spilling.
+#ifndef CUZFP_F64_ENC_WAVES
+#define CUZFP_F64_ENC_WAVES 3
+#endif
+template <typename Scalar, int DIMS, bool ENC = false> struct occupancy {
+  static constexpr int value = (sizeof(Scalar) == 8 && DIMS == 3) ? (ENC ? CUZFP_F64_ENC_WAVES : 2) : 4;
 };
 
 template <typename Scalar, int DIMS, bool FAST, bool ALIGNED, bool PRIO = true>
-__global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::value)) void zfp_encode(const Scalar* __restrict__ data,
+__global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS, true>::value)) void zfp_encode(const Scalar* __restrict__ data,
                                                                       Geometry g,
                                                                       uint64_t* __restrict__ stream) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds_all[];
@@ -468,7 +493,11 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
   // W words per block plus kSlackWords rows
   const uint32_t W = g.maxbits >> 6;
   Scalar f[N];
+#if defined(CUZFP_EXP_NOLOAD)  // timing experiment (tools/variants.py): a synthetic smooth block, no HBM reads
+  for (int i = 0; i < N; i++) f[i] = (Scalar)(1.0f + 0.001f * (float)((b & 255) + 3 * i + (i >> 2) * (i & 3)));
+#else
   if (b < g.nblocks) gather<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
+#endif
   ((uint4*)lut)[lane] = spread16;  // every lane: the table is the wave's
   if (b < g.nblocks) {
     if constexpr (ALIGNED) {
@@ -634,7 +663,15 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
     }
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);  // a wave out of the coder stores at once
     if (coded) {
+#if defined(CUZFP_EXP_NOSTORE)  // timing experiment: one value a block reaches HBM
+      {
+        Scalar acc = f[0];
+        for (int i = 1; i < N; i++) acc += f[i];
+        if (acc == (Scalar)1234.5678) data[b] = acc;
+      }
+#else
       scatter<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
+#endif
     } else {  // a zero block
       Scalar z[N];
 #pragma unroll
@@ -696,7 +733,7 @@ int launch_encode_t(const void* data, const Geometry& g, bool fast, uint64_t* st
   const dim3 grid((nwaves + wpg - 1) / wpg), block(kLanes * wpg);
   const size_t lds = (size_t)wpg * (gg.lds_words * 8 + kSpreadLutBytes);
   const Scalar* d = (const Scalar*)data;
-  if (fast && aligned && !use_priority(nwaves, occupancy<Scalar, DIMS>::value, 1))
+  if (fast && aligned && !use_priority(nwaves, occupancy<Scalar, DIMS, true>::value, 1))
     hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, true, true, false>), grid, block, lds, st, d, gg, stream);
   else if (fast && aligned)
     hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, true, true>), grid, block, lds, st, d, gg, stream);

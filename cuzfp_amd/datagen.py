@@ -11,6 +11,9 @@
   worst case for the plane coder).
 * :func:`ramp` -- ``f[i] = i``, the input of the reference's sanity tests
   (src/tests/t_sanity_check_{1,2,3}.cpp).
+* :func:`sine_field` -- ``f[x] = (T)(sin(x * 3.14/180) * 10)``, the input of
+  the reference's 1D encode/decode test (src/tests/t_encode_decode_1.cpp:15-30),
+  BASELINE.json configs[0] at 1M values.
 
 Shapes are numpy order (slowest first).
 """
@@ -57,6 +60,19 @@ def polynomial_slab(global_shape, z0: int, z1: int, dtype=np.float32) -> np.ndar
     return np.ascontiguousarray(f.astype(dtype, copy=False))
 
 
+def polynomial_slab_device(gshape, z0: int, z1: int, device):
+    """datagen.polynomial_slab built on the GPU: the three 1D axes come from the
+    CPU generator (testzfp's IEEE op order) and the two products are exact-
+    rounded f32 multiplies on the device, so the slab is bit-identical (the
+    stream hash against the reference's checks it)."""
+    import torch
+    nz, ny, nx = gshape
+    fx = torch.from_numpy(_axis(nx, np.float32)).to(device)
+    fy = torch.from_numpy(_axis(ny, np.float32)).to(device)
+    fz = torch.from_numpy(_axis(nz, np.float32)[z0:z1].copy()).to(device)
+    return ((fx[None, :] * fy[:, None])[None, :, :] * fz[:, None, None]).contiguous()
+
+
 def splitmix64(n: int, seed: int = 42) -> np.ndarray:
     """n successive outputs of splitmix64 seeded with `seed`."""
     with np.errstate(over="ignore"):
@@ -81,3 +97,10 @@ def splitmix_uniform(shape, dtype=np.float32, seed: int = 42) -> np.ndarray:
 
 def ramp(shape, dtype=np.float32) -> np.ndarray:
     return np.arange(int(np.prod(shape)), dtype=dtype).reshape(shape)
+
+
+def sine_field(n: int, dtype=np.float32) -> np.ndarray:
+    """src/tests/t_encode_decode_1.cpp:18-23: v = x * (3.14/180.) in double,
+    value = (T)(sin(v) * 10.)."""
+    v = np.arange(n, dtype=np.float64) * (3.14 / 180.0)
+    return (np.sin(v) * 10.0).astype(dtype)

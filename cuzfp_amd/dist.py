@@ -78,5 +78,49 @@ def stream_offset_words(shape, world: int, rank: int, maxbits: int) -> int:
     return rank * segment_words(shape, world, maxbits)
 
 
-__all__ = ["slab_extent", "blocks_per_slab", "uniform_shard_ok", "segment_words",
+class StrongShard:
+    """Rank `rank`'s share of one E^3 array sharded over `world` ranks as z-slabs
+    of E/world planes (BASELINE configs[4]: E = 1024, world = 8): its slab of
+    the global array, the local shape and its word range in the global stream."""
+
+    def __init__(self, edge: int, world: int, rank: int, maxbits: int):
+        if edge % (4 * world):
+            raise ValueError(f"edge {edge} is not a multiple of 4 * world ({world})")
+        self.edge, self.world, self.rank, self.maxbits = edge, world, rank, maxbits
+        self.global_shape = (edge, edge, edge)
+        self.z0 = rank * edge // world
+        self.z1 = (rank + 1) * edge // world
+        self.shape = (self.z1 - self.z0, edge, edge)
+        if not uniform_shard_ok(self.global_shape, world, maxbits):
+            raise ValueError("segments are not whole 64-bit words")
+        self.words = segment_words(self.global_shape, world, maxbits)
+        self.word0 = stream_offset_words(self.global_shape, world, rank, maxbits)
+        self.values = self.shape[0] * edge * edge
+
+
+def sharded_summary(shard: "StrongShard", itemsize: int, step_s: float, enc_s: list, dec_s: list,
+                    hbm_peak_GBps: float, allgather_s: float | None = None) -> dict:
+    """The bench line's record of one strong-scaled sharded run: `step_s` is the
+    max over ranks of one encode+decode step, enc_s / dec_s the per-rank kernel
+    times (seconds), allgather_s the max-over-ranks all-gather time."""
+    g_in = shard.edge ** 3 * itemsize                 # global input bytes
+    stream = shard.words * 8 * shard.world            # global stream bytes
+    algo = 2 * (g_in + stream)                        # read + write, both kernels, all ranks
+    out = {"workload": f"3d_float32_{shard.edge}^3_rate{shard.maxbits / 64:g}_zslab{shard.world}",
+           "n_ranks": shard.world, "slab_shape": list(shard.shape), "global_shape": list(shard.global_shape),
+           "maxbits": shard.maxbits, "step_ms": round(step_s * 1e3, 4),
+           "value_GBps": round(g_in / step_s / 1e9, 2),
+           "frac_of_aggregate_hbm": round(algo / step_s / 1e9 / (hbm_peak_GBps * shard.world), 4),
+           "encode_ms_per_rank": [round(t * 1e3, 4) for t in enc_s],
+           "decode_ms_per_rank": [round(t * 1e3, 4) for t in dec_s],
+           "stream_bytes": stream}
+    if allgather_s is not None:
+        recv = stream - shard.words * 8               # bytes each rank receives
+        out["allgather"] = {"ms": round(allgather_s * 1e3, 4), "bytes_in_per_rank": recv,
+                            "GBps_in_per_rank": round(recv / allgather_s / 1e9, 2) if allgather_s > 0 else None,
+                            "backend": "nccl (RCCL)"}
+    return out
+
+
+__all__ = ["StrongShard", "sharded_summary", "slab_extent", "blocks_per_slab", "uniform_shard_ok", "segment_words",
            "local_shape", "allgather_stream", "stream_offset_words"]

@@ -112,6 +112,12 @@ int cuzfp_hip_decompress_host(const void* h_stream, size_t stream_bytes, int typ
                               unsigned nx, unsigned ny, unsigned nz, unsigned maxbits,
                               void* h_data, int nstreams);
 
+/* Diagnostic, not a reference entry point: device-to-device copy of `bytes`
+ * (a multiple of 16, both pointers 16-byte aligned) with 16-byte non-temporal
+ * loads and stores -- the codec's access width and cache policy.  bench.py
+ * times it as the achievable-HBM-bandwidth calibrator. */
+int cuzfp_hip_copy(const void* d_src, void* d_dst, size_t bytes, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

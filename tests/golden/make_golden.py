@@ -16,7 +16,8 @@ Outputs (all data, no reference source):
                reference stream and of its decompressed array, max abs error;
                plus the same for seeded splitmix64 fuzz cases (the dims/rate space
                of src/utils/test.py:101-132) and for BASELINE.json's full-size
-               configurations (hashes only).
+               configurations (hashes only), including configs[4]'s 1024^3
+               array with the word-range hashes of its z-slab shards.
 """
 from __future__ import annotations
 
@@ -71,7 +72,36 @@ def case(ref, a: np.ndarray, maxbits: int, keep_stream: bool):
     return rec, (s if keep_stream else None)
 
 
+def add_sharded_1024(golden: dict, ref) -> None:
+    """BASELINE configs[4]: the 1024^3 f32 polynomial field at rate 8, the array
+    the bench shards over N GPUs as z-slabs of 1024/N planes.  Hashes of the
+    whole stream, of its N equal word ranges (N = 2, 4, 8: rank r's slab
+    encodes to words [r*W/N, (r+1)*W/N)) and of the decoded array."""
+    shape, dt, rate = (1024, 1024, 1024), np.float32, 8
+    a = polynomial_field(shape, dt)
+    mb = ref.rate_to_maxbits(rate, dt, 3)
+    s = ref.compress(a, mb)
+    d = ref.decompress(s, shape, dt, mb)
+    rec = {"shape": list(shape), "dtype": "float32", "maxbits": int(mb), "bytes": int(s.nbytes),
+           "stream_sha256": sha(s), "decoded_sha256": sha(d), "rate": rate, "generator": "polynomial",
+           "max_abs_err": float(np.max(np.abs(d.astype(np.float64) - a.astype(np.float64))))}
+    for n in (2, 4, 8):
+        w = s.size // n
+        rec[f"slab_sha256_n{n}"] = [sha(s[r * w:(r + 1) * w]) for r in range(n)]
+    golden["cases"]["baseline/3d_f32_1024_r8/polynomial"] = rec
+    print("baseline/3d_f32_1024_r8", rec["bytes"], rec["max_abs_err"], flush=True)
+
+
 def main() -> None:
+    if "--only-1024" in sys.argv:  # append configs[4] to an existing golden.json
+        oracle.build(with_reference=True)
+        oracle.reload()
+        path = os.path.join(HERE, "golden.json")
+        golden = json.load(open(path))
+        add_sharded_1024(golden, oracle.reference)
+        with open(path, "w") as f:
+            json.dump(golden, f, indent=1, sort_keys=True)
+        return
     oracle.build(with_reference=True)
     oracle.reload()
     ref = oracle.reference
@@ -134,6 +164,8 @@ def main() -> None:
             rec.update({"rate": rate, "generator": gen, "seed": 42})
             golden["cases"][f"{name}/{gen}"] = rec
             print(name, gen, rec["bytes"], rec["max_abs_err"], flush=True)
+
+    add_sharded_1024(golden, ref)
 
     np.savez_compressed(os.path.join(HERE, "streams.npz"), **{k.replace("/", "__"): v
                                                                for k, v in streams.items()})

@@ -131,3 +131,72 @@ def test_gpu_slabs_allgather(restatement):
         assert np.array_equal(results[r][0], want)
         z0, z1 = zd.slab_extent(shape[0], world, r)
         assert np.array_equal(results[r][1], back[z0:z1])
+
+
+def _config5_worker(rank, world, port, edge, q):
+    # bench.py's configs[4] bookkeeping on CPU: StrongShard's slab and word
+    # range, the oracle standing in for the kernels, the gloo all-gather, the
+    # max-over-ranks reductions and sharded_summary's record
+    import torch
+    import torch.distributed as dist
+    import oracle
+    from cuzfp_amd import dist as zd
+    from cuzfp_amd.datagen import polynomial_slab
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sh = zd.StrongShard(edge, world, rank, 512)
+        local = polynomial_slab(sh.global_shape, sh.z0, sh.z1, np.float32)
+        assert local.shape == sh.shape
+        words = oracle.restatement.compress(local, 512).view(np.int64)
+        assert words.size == sh.words
+        full = zd.allgather_stream(torch.from_numpy(words.copy()))
+        t = torch.tensor([0.001 * (rank + 1)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        rec = zd.sharded_summary(sh, 4, float(t.item()), [0.0004] * world, [0.0005] * world, 8000.0, 0.0002)
+        q.put((rank, sh.word0, full.numpy().view(np.uint64).copy(), rec))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_config5_bookkeeping_gloo(restatement):
+    """Two gloo ranks run bench.py's configs[4] path on a 32^3 array: each
+    rank's slab encodes to its word range of the one-process stream, the
+    all-gather rebuilds that stream on both ranks, and the summary's step
+    time is the max over ranks."""
+    import multiprocessing as mp
+    from cuzfp_amd import dist as zd
+    from cuzfp_amd.datagen import polynomial_field
+    edge, world = 32, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_config5_worker, args=(r, world, port, edge, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict((r, (w0, full, rec)) for r, w0, full, rec in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = restatement.compress(polynomial_field((edge,) * 3, np.float32), 512)
+    seg = want.size // world
+    for r in range(world):
+        w0, full, rec = got[r]
+        assert w0 == r * seg
+        assert np.array_equal(full, want)
+        assert rec["step_ms"] == 2.0 and rec["n_ranks"] == world and rec["slab_shape"] == [edge // world, edge, edge]
+        assert rec["stream_bytes"] == want.nbytes
+        assert rec["allgather"]["bytes_in_per_rank"] == want.nbytes // world
+        assert rec["value_GBps"] == round(edge ** 3 * 4 / 0.002 / 1e9, 2)
+
+
+def test_strong_shard_ranges():
+    from cuzfp_amd import dist as zd
+    for world in (1, 2, 4, 8):
+        shards = [zd.StrongShard(1024, world, r, 512) for r in range(world)]
+        assert sum(s.words for s in shards) == 1024 ** 3 // 64 * 512 // 64
+        assert [s.word0 for s in shards] == [r * shards[0].words for r in range(world)]
+        assert shards[-1].z1 == 1024 and all(s.shape[0] == 1024 // world for s in shards)
+    with pytest.raises(ValueError):
+        zd.StrongShard(1024, 3, 0, 512)

@@ -414,3 +414,47 @@ def test_largest_maxbits(cuda, restatement, dims, dtype):
         ref = restatement.compress(a, mb)
         assert np.array_equal(words, ref), mb
         assert np.array_equal(y, restatement.decompress(ref, shape, dtype, mb)), mb
+
+
+def _golden_1024():
+    import json
+    import os
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "golden.json")
+    return json.load(open(path))["cases"]["baseline/3d_f32_1024_r8/polynomial"]
+
+
+@pytest.mark.timeout(600)
+def test_golden_1024_full_array(cuda):
+    """BASELINE configs[4]'s whole 1024^3 array on one GPU: the stream and the
+    decoded array against the reference's SHA-256s (tests/golden/golden.json,
+    made from the compiled reference by make_golden.py)."""
+    import hashlib
+    import torch
+    from cuzfp_amd.datagen import polynomial_slab_device
+    gold = _golden_1024()
+    x = polynomial_slab_device((1024, 1024, 1024), 0, 1024, cuda)
+    mb = cz.rate_to_maxbits(8, np.float32, 3)
+    words = cz.encode(x, mb)
+    y = cz.decode(words, x.shape, x.dtype, mb)
+    torch.cuda.synchronize()
+    assert hashlib.sha256(words.cpu().numpy().tobytes()).hexdigest() == gold["stream_sha256"]
+    del x, words
+    assert hashlib.sha256(y.cpu().numpy().tobytes()).hexdigest() == gold["decoded_sha256"]
+
+
+@pytest.mark.parametrize("world,rank", [(8, 0), (8, 7), (4, 2), (2, 1)])
+def test_golden_1024_slab(cuda, world, rank):
+    """One rank's z-slab of the 1024^3 array (1024/N planes) encodes to exactly
+    its word range of the reference's stream: [r*W/N, (r+1)*W/N)."""
+    import hashlib
+    import torch
+    from cuzfp_amd import dist as zd
+    from cuzfp_amd.datagen import polynomial_slab_device
+    gold = _golden_1024()
+    mb = cz.rate_to_maxbits(8, np.float32, 3)
+    sh = zd.StrongShard(1024, world, rank, mb)
+    x = polynomial_slab_device(sh.global_shape, sh.z0, sh.z1, cuda)
+    words = cz.encode(x, mb)
+    torch.cuda.synchronize()
+    assert words.numel() == sh.words
+    assert hashlib.sha256(words.cpu().numpy().tobytes()).hexdigest() == gold[f"slab_sha256_n{world}"][rank]
