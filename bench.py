@@ -403,7 +403,7 @@ def main():
 
     hbm_copy = None
     if rank == 0 and not args.no_copy_probe:
-        hbm_copy = {"kernel": "cuzfp_hip_copy (16-B non-temporal loads/stores, 4 in flight a lane)",
+        hbm_copy = {"kernel": "cuzfp_hip_copy (16-B non-temporal loads/stores, one per lane, one grid)",
                     "GBps_1GiB": copy_GBps(1 << 30, "cuzfp"), "GBps_at_input_size": copy_GBps(a.nbytes, "cuzfp"),
                     "torch_copy_GBps_1GiB": copy_GBps(1 << 30, "torch"), "input_bytes": a.nbytes,
                     "note": "read + write bytes / time, hipGraph of 10 copies; at the input size source and "

@@ -286,27 +286,21 @@ static int host_pipeline(const Problem& p, bool encode, void* h_data, void* h_st
 
 // ---------------------------------------------------------------------------
 // Bandwidth calibrator (cuzfp_hip_copy): a device-to-device copy with 16-byte
-// non-temporal loads and stores, four in flight per lane, the codec's own
-// access width and cache policy.  bench.py times it at 1 GiB beside the codec
-// as the achievable-HBM reference (roofline.frac_of_copy).
+// non-temporal loads and stores, one per lane, one grid over the whole buffer
+// -- the codec's own access width, cache policy and one-touch-per-wave shape.
+// bench.py times it at 1 GiB beside the codec as the achievable-HBM reference
+// (roofline.frac_of_copy).  tools/ubench/copy.hip (profiles/r02_copy_ubench.txt):
+// this shape 6.64 TB/s (read + write) at 1 GiB; grid-stride loops over
+// 1-32 workgroups per CU with 1-8 accesses in flight a lane 4.6-6.4 TB/s;
+// plain (temporal) accesses 0.3-0.5 TB/s below non-temporal.
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __global__ __launch_bounds__(256) void copy16_nt(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
                                                  size_t n16) {
   const size_t stride = (size_t)gridDim.x * blockDim.x;
-  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (; i + 3 * stride < n16; i += 4 * stride) {
-    const u32x4 a = __builtin_nontemporal_load(src + i);
-    const u32x4 b = __builtin_nontemporal_load(src + i + stride);
-    const u32x4 c = __builtin_nontemporal_load(src + i + 2 * stride);
-    const u32x4 d = __builtin_nontemporal_load(src + i + 3 * stride);
-    __builtin_nontemporal_store(a, dst + i);
-    __builtin_nontemporal_store(b, dst + i + stride);
-    __builtin_nontemporal_store(c, dst + i + 2 * stride);
-    __builtin_nontemporal_store(d, dst + i + 3 * stride);
-  }
-  for (; i < n16; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride)
+    __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
 }
 
 }  // namespace cuzfp
@@ -388,13 +382,8 @@ int cuzfp_hip_copy(const void* d_src, void* d_dst, size_t bytes, hipStream_t str
   if (!d_src || !d_dst || (bytes & 15) || (((uintptr_t)d_src | (uintptr_t)d_dst) & 15))
     return CUZFP_ERROR_INVALID_ARGUMENT;
   if (!bytes) return CUZFP_SUCCESS;
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    cus = 256;
   const size_t n16 = bytes / 16;
-  const size_t want = (n16 + 255) / 256;
-  const unsigned grid = (unsigned)std::min<size_t>(want, (size_t)cus * 8);
+  const unsigned grid = (unsigned)std::min<size_t>((n16 + 255) / 256, 1u << 30);
   hipLaunchKernelGGL(copy16_nt, dim3(grid), dim3(256), 0, stream, (const u32x4*)d_src, (u32x4*)d_dst, n16);
   const hipError_t e = hipGetLastError();
   t_last_hip = e;

@@ -454,10 +454,12 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 // Waves per SIMD the register budget is sized for: 4 (<= 128 VGPRs) in
 // general.  3D double blocks hold 64 x 64-bit values (128 VGPRs) and then 64 x
-// 64-bit planes: the encoder fits 3 waves (<= 168 VGPRs), the decoder, whose
-// plane loop keeps more state live, 2 (<= 256) rather than spilling.
+// 64-bit planes, so 2 (<= 256 VGPRs) rather than spilling.  At 3 waves
+// (<= 168) the encoder spills 40 B a lane and the decoder 268 B; the encoder at
+// 3 measured 66.7 us against 56.7 us at 2 (256^3 rate 16, tools/variants.py
+// f64w3 / f64w2), so CUZFP_F64_ENC_WAVES stays 2.
 #ifndef CUZFP_F64_ENC_WAVES
-#define CUZFP_F64_ENC_WAVES 3
+#define CUZFP_F64_ENC_WAVES 2
 #endif
 template <typename Scalar, int DIMS, bool ENC = false> struct occupancy {
   static constexpr int value = (sizeof(Scalar) == 8 && DIMS == 3) ? (ENC ? CUZFP_F64_ENC_WAVES : 2) : 4;
