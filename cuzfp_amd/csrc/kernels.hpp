@@ -208,10 +208,18 @@ struct LdsReader {
     return;
 #endif
     const uint32_t base = (uint32_t)(uintptr_t)(lds_u32*)lut32;
-    const uint32_t c1 = group ? (g & kChunkMask) : kNoGroupEntry - (2u << kChunkBits);
+    // A lane whose leading group test reads "0" (no new ones: about half the
+    // lane-steps) looks up entry 0 for both chunks -- the same "0" entry as
+    // any even chunk, and a chunk 2 that is dropped anyway -- so those lanes'
+    // reads are broadcasts instead of bank conflicts (random entries made 51 %
+    // of the decoder's LDS cycles conflict cycles, SQ_LDS_BANK_CONFLICT).
+    uint32_t t;
+    asm("v_bfe_i32 %0, %1, 0, 1" : "=v"(t) : "v"(g));  // -(leading test bit)
+    const uint32_t gm = g & t;
+    const uint32_t c1 = group ? (gm & kChunkMask) : kNoGroupEntry - (2u << kChunkBits);
     uint32_t a1, c2, a2;
     asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a1) : "v"(c1), "s"(base));
-    asm("v_bfe_u32 %0, %1, %2, %2" : "=v"(c2) : "v"(g), "i"(kChunkBits));
+    asm("v_bfe_u32 %0, %1, %2, %2" : "=v"(c2) : "v"(gm), "i"(kChunkBits));
     asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a2) : "v"(c2), "s"(base));
     e1 = ((lds_u32*)(uintptr_t)a1)[2u << kChunkBits];
     e2a = ((lds_u32*)(uintptr_t)a2)[0];
@@ -237,7 +245,9 @@ struct LdsReader {
   }
   __device__ __forceinline__ uint32_t chunk1(uint32_t g, bool group) const {
     const uint32_t base = (uint32_t)(uintptr_t)(lds_u32*)lut32;
-    const uint32_t c1 = group ? (g & kChunkMask) : kNoGroupEntry - (2u << kChunkBits);
+    uint32_t t;
+    asm("v_bfe_i32 %0, %1, 0, 1" : "=v"(t) : "v"(g));  // "0" leading test: entry 0 (see chunks)
+    const uint32_t c1 = group ? (g & t & kChunkMask) : kNoGroupEntry - (2u << kChunkBits);
     uint32_t a1;
     asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a1) : "v"(c1), "s"(base));
     return ((lds_u32*)(uintptr_t)a1)[2u << kChunkBits];
