@@ -225,6 +225,23 @@ struct LdsReader {
     e2a = ((lds_u32*)(uintptr_t)a2)[0];
     e2b = ((lds_u32*)(uintptr_t)a2)[1u << kChunkBits];
   }
+  // the fast step's lookups: as chunks(), with n = N-1 (last) taking the two
+  // last-position entries by the group test bit instead of a chunk
+  __device__ __forceinline__ void chunks_fast(uint32_t g, bool last, uint32_t& e1, uint32_t& e2a,
+                                              uint32_t& e2b) const {
+    const uint32_t base = (uint32_t)(uintptr_t)(lds_u32*)lut32;
+    uint32_t t;
+    asm("v_bfe_i32 %0, %1, 0, 1" : "=v"(t) : "v"(g));  // "0" leading test: entry 0 (see chunks)
+    const uint32_t gm = g & t;
+    const uint32_t c1 = last ? ((kLastPosEntry - (2u << kChunkBits)) | (g & 1u)) : (gm & kChunkMask);
+    uint32_t a1, c2, a2;
+    asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a1) : "v"(c1), "s"(base));
+    asm("v_bfe_u32 %0, %1, %2, %2" : "=v"(c2) : "v"(gm), "i"(kChunkBits));
+    asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a2) : "v"(c2), "s"(base));
+    e1 = ((lds_u32*)(uintptr_t)a1)[2u << kChunkBits];
+    e2a = ((lds_u32*)(uintptr_t)a2)[0];
+    e2b = ((lds_u32*)(uintptr_t)a2)[1u << kChunkBits];
+  }
   // continuation pairs (dense planes): 32 stream bits at bit q of the block,
   // chunk A in state st (0/1), chunk B in states 0 and 1
   __device__ __forceinline__ uint32_t window32(uint32_t q) const {
@@ -242,6 +259,15 @@ struct LdsReader {
     eA = ((lds_u32*)(uintptr_t)aA)[0];
     eBa = ((lds_u32*)(uintptr_t)a2)[0];
     eBb = ((lds_u32*)(uintptr_t)a2)[1u << kChunkBits];
+  }
+  __device__ __forceinline__ uint32_t chunk1_fast(uint32_t g, bool last) const {
+    const uint32_t base = (uint32_t)(uintptr_t)(lds_u32*)lut32;
+    uint32_t t;
+    asm("v_bfe_i32 %0, %1, 0, 1" : "=v"(t) : "v"(g));  // "0" leading test: entry 0 (see chunks)
+    const uint32_t c1 = last ? ((kLastPosEntry - (2u << kChunkBits)) | (g & 1u)) : (g & t & kChunkMask);
+    uint32_t a1;
+    asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a1) : "v"(c1), "s"(base));
+    return ((lds_u32*)(uintptr_t)a1)[2u << kChunkBits];
   }
   __device__ __forceinline__ uint32_t chunk1(uint32_t g, bool group) const {
     const uint32_t base = (uint32_t)(uintptr_t)(lds_u32*)lut32;

@@ -1047,6 +1047,7 @@ constexpr uint32_t kUsedMask = (1u << 14) - 1, kNotEnded = 1u << 13;
 constexpr uint32_t kEntryState = 1u << 31;
 // a last entry, for planes with no group part (n = N): ended, nothing used
 constexpr uint32_t kNoGroupEntry = 3u << kChunkBits;
+constexpr uint32_t kLastPosEntry = kNoGroupEntry + 2;  // and + 1
 
 constexpr uint32_t pack_entry(uint32_t ones, uint32_t pos, uint32_t used, uint32_t flags) {
   return (ones << kOnesShift) | (pos << kPosShift) | used | flags;
@@ -1091,6 +1092,11 @@ constexpr ChunkLut make_chunk_lut() {
   for (unsigned s = 0; s < 3; s++)
     for (uint32_t b = 0; b <= kChunkMask; b++) t.e[(s << kChunkBits) | b] = chunk_entry(s, b);
   t.e[kNoGroupEntry] = pack_entry(0, 0, 0, 0);
+  // n = N-1 (the fast decoder keeps n at most N-1): the group part is the
+  // last position's bit alone -- a "0" test, or a "1" test with the one at
+  // N-1 implied -- indexed by that bit (decode_plane_fast)
+  t.e[kLastPosEntry] = pack_entry(0, 0, 1, 0);
+  t.e[kLastPosEntry + 1] = pack_entry(1, 0, 1, 0);
   return t;
 }
 
@@ -1134,11 +1140,15 @@ ZFP_HD uint32_t drop_if_bit13(uint32_t v, uint32_t e) {
 template <int DIMS, typename PW, typename Reader>
 ZFP_HD PW decode_plane_lut(unsigned& bits, unsigned& n, Reader& rd, bool& slow) {
   constexpr unsigned N = 1u << (2 * DIMS);
-  const unsigned m = umin(n, bits);
+  // n is kept at most N-1: with n = N-1 the group part is the last
+  // position's bit alone (a "0" test, or a "1" test with the one implied),
+  // which reads the same bits as N verbatim ones; two dedicated table entries
+  // decode it (kLastPosEntry)
+  const unsigned nf = n < N - 1 ? n : N - 1;
+  const unsigned m = umin(nf, bits);
   uint64_t w;
   uint32_t g;
   rd.windows(m, w, g);
-  const uint64_t vmask = lowmask64(m);
   const unsigned b1 = bits - m;                // budget after the verbatim bits
   // chunk 1 starts at the leading group test (table state 2), chunk 2 is read
   // in both states and chosen by chunk 1's exit state; nothing follows a
@@ -1146,11 +1156,11 @@ ZFP_HD PW decode_plane_lut(unsigned& bits, unsigned& n, Reader& rd, bool& slow) 
   uint32_t e1, e2;
   if constexpr (DIMS == 1) {
     // a 1D code (4 positions, at most 7 bits with the leading test) fits chunk 1
-    e1 = rd.chunk1(g, n < N);
+    e1 = rd.chunk1_fast(g, nf == N - 1);
     e2 = 0;
   } else {
     uint32_t e2a, e2b;
-    rd.chunks(g, n < N, e1, e2a, e2b);
+    rd.chunks_fast(g, nf == N - 1, e1, e2a, e2b);
     const uint32_t e2s = (e1 & kEntryState) ? e2b : e2a;
     e2 = keep_if_bit13(e2s, e1);  // nothing after a chunk 1 that ended
   }
@@ -1165,12 +1175,13 @@ ZFP_HD PW decode_plane_lut(unsigned& bits, unsigned& n, Reader& rd, bool& slow) 
   // (its zero group test is not in the stream): the reference keeps that one
   // and reads no more (decode.c:302-317).  Codes longer than the two chunks
   // and codes the budget cuts short take decode_plane_cont; a code reaching
-  // position N-1 the general decoder.  (N - 1 - n is huge for n = N.)
-  slow = !(used <= b1 + 1 && npos <= N - 1 - n);
+  // position N-1 the general decoder.
+  slow = !(used <= b1 + 1 && npos <= N - 1 - nf);
   // the verbatim bits below m, the new ones at n >= m: one v_bfi_b32 a dword
-  const PW o = (PW)ones << (n & (8 * sizeof(PW) - 1));
-  const PW x = ((PW)vmask & (PW)w) | (~(PW)vmask & o);
-  n += npos;
+  // under the mask ~0 << m (m <= N-1)
+  const PW hi = (PW)(~0ull << m);
+  const PW x = (hi & ((PW)ones << nf)) | (~hi & (PW)w);
+  n = nf + npos;
   const unsigned adv = m + umin(used, b1);
   rd.pos += adv;
   bits -= adv;
@@ -1272,6 +1283,46 @@ ZFP_HD PW decode_plane_cont(unsigned& bits, unsigned& n, Reader& rd, bool& slow)
   return x;
 }
 
+// Table step without the budget (the decoder's common case, 3D): when every
+// lane of the wave has budget for the plane's longest table-decodable code
+// (N-1 verbatim bits + a two-chunk group code), the reads need no clipping
+// and no lane's budget can end inside the plane.  n is kept at most N-1 (with
+// n = N-1 the group part is the last position's bit alone, looked up in two
+// dedicated entries), so the verbatim mask is one shift.  Sets `slow` for a
+// code longer than two chunks or one reaching position N-1; the caller then
+// decodes that plane again with the budget-aware steps.
+template <int DIMS, typename PW, typename Reader>
+ZFP_HD PW decode_plane_fast(unsigned& bits, unsigned& n, Reader& rd, bool& slow) {
+  constexpr unsigned N = 1u << (2 * DIMS);
+  const unsigned nf = n < N - 1 ? n : N - 1;
+  uint64_t w;
+  uint32_t g;
+  rd.windows(nf, w, g);
+  uint32_t e1, e2a, e2b;
+  rd.chunks_fast(g, nf == N - 1, e1, e2a, e2b);
+  const uint32_t e2 = keep_if_bit13((e1 & kEntryState) ? e2b : e2a, e1);
+  const uint32_t S = e1 + e2;
+  const uint32_t npos = S >> kPosShift & 31u;
+  const uint32_t used = S & kUsedMask;
+  const uint32_t ones = ((e1 >> kOnesShift) & kChunkMask) |
+                        (((e2 >> kOnesShift) & kChunkMask) << ((e1 >> kPosShift) & 31u));
+  slow = used >= kNotEnded || npos > N - 1 - nf;
+  // bits >= nf of the plane from the group code, below it verbatim: one
+  // v_bfi_b32 a dword under the mask ~0 << nf
+  const PW hi = (PW)(~0ull << nf);
+  const PW x = (hi & ((PW)ones << nf)) | (~hi & (PW)w);
+  n = nf + npos;
+  const unsigned adv = nf + used;
+  rd.pos += adv;
+  bits -= adv;
+  return x;
+}
+
+// Budget for two fast steps: 2 x (N-1 verbatim + 21 group bits)
+template <int DIMS> struct fast_room {
+  static constexpr unsigned value = 2u * ((1u << (2 * DIMS)) - 1u + 21u);
+};
+
 // Plane loop: the table decoder for every lane, then, only when some lane of
 // the wave needs it, the general decoder for those lanes.
 template <int DIMS, typename PW, typename Reader>
@@ -1281,6 +1332,33 @@ ZFP_HD PW decode_plane_any(unsigned& bits, unsigned& n, Reader& rd) {
   bool slow;
   PW x = decode_plane_lut<DIMS, PW>(bits, n, rd, slow);
   if (__builtin_expect(any_lane(slow), 0)) {  // wave-uniform test first (see encode_plane_any)
+    if (slow) {
+      rd.init(pos0);
+      n = n0;
+      bits = bits0;
+      x = decode_plane_cont<DIMS, PW>(bits, n, rd, slow);
+    }
+    if (__builtin_expect(any_lane(slow), 0)) {
+      if (slow) {
+        rd.init(pos0);
+        n = n0;
+        bits = bits0;
+        x = decode_plane<DIMS, PW>(bits, n, rd);
+      }
+    }
+  }
+  return x;
+}
+
+// The fast step with its fallbacks (the budget-aware steps) for the lanes
+// that need them.
+template <int DIMS, typename PW, typename Reader>
+ZFP_HD PW decode_plane_fast_any(unsigned& bits, unsigned& n, Reader& rd) {
+  const auto pos0 = rd.pos;
+  const unsigned n0 = n, bits0 = bits;
+  bool slow;
+  PW x = decode_plane_fast<DIMS, PW>(bits, n, rd, slow);
+  if (__builtin_expect(any_lane(slow), 0)) {
     if (slow) {
       rd.init(pos0);
       n = n0;
@@ -1310,8 +1388,14 @@ ZFP_HD int decode_half(planes<UInt, DIMS>& P, unsigned& bits, unsigned& n, int c
     if (!any_lane(bits != 0)) return c;
     if constexpr (prio_of<Reader>::value)
       progress_priority<CUZFP_DPRIO_T2, CUZFP_DPRIO_T1, CUZFP_DPRIO_T0>(uniform(c));
-    const PW xa = decode_plane_any<DIMS, PW>(bits, n, rd);
-    const PW xb = decode_plane_any<DIMS, PW>(bits, n, rd);
+    PW xa, xb;
+    if (DIMS == 3 && !any_lane(bits < fast_room<DIMS>::value)) {
+      xa = decode_plane_fast_any<DIMS, PW>(bits, n, rd);
+      xb = decode_plane_fast_any<DIMS, PW>(bits, n, rd);
+    } else {
+      xa = decode_plane_any<DIMS, PW>(bits, n, rd);
+      xb = decode_plane_any<DIMS, PW>(bits, n, rd);
+    }
     const int u = uniform(c);
     P.template set<H>(u, xa);
     P.template set<H>(u - 1, xb);

@@ -85,6 +85,18 @@ struct HostReader {
     e2a = t[c2];
     e2b = t[c2 + (1u << cuzfp::kChunkBits)];
   }
+  void chunks_fast(uint32_t g, bool last, uint32_t& e1, uint32_t& e2a, uint32_t& e2b) const {
+    const uint32_t* t = table().e;
+    const uint32_t gm = (g & 1u) ? g : 0u;
+    const uint32_t c2 = (gm >> cuzfp::kChunkBits) & cuzfp::kChunkMask;
+    e1 = t[last ? cuzfp::kLastPosEntry + (g & 1u) : (2u << cuzfp::kChunkBits) | (gm & cuzfp::kChunkMask)];
+    e2a = t[c2];
+    e2b = t[c2 + (1u << cuzfp::kChunkBits)];
+  }
+  uint32_t chunk1_fast(uint32_t g, bool last) const {
+    const uint32_t gm = (g & 1u) ? g : 0u;
+    return table().e[last ? cuzfp::kLastPosEntry + (g & 1u) : (2u << cuzfp::kChunkBits) | (gm & cuzfp::kChunkMask)];
+  }
   uint32_t chunk1(uint32_t g, bool group) const {
     return table().e[group ? (2u << cuzfp::kChunkBits) | (g & cuzfp::kChunkMask) : cuzfp::kNoGroupEntry];
   }
@@ -230,7 +242,15 @@ extern "C" long long emu_fuzz_plane(unsigned long long seed, long long trials, i
       xa = cuzfp::decode_plane_any<1, uint32_t>(ba, na, ra);
       xb = cuzfp::decode_plane<1, uint32_t>(bb, nb, rb);
     }
-    if (xa != xb || na != nb || ba != bb || ra.pos != rb.pos) bad++;
+    // n = N-1 and n = N are the same state (the table steps keep n <= N-1)
+    auto cap = [&](unsigned v) { return v < N - 1 ? v : N - 1; };
+    if (xa != xb || cap(na) != cap(nb) || ba != bb || ra.pos != rb.pos) bad++;
+    if (dims == 3 && bits0 >= cuzfp::fast_room<3>::value / 2) {  // the budget-free step (decode_half's fast pairs)
+      HostReader rc{buf, 6, 0, end};
+      unsigned nc = n0, bc = bits0;
+      const uint64_t xc = cuzfp::decode_plane_fast_any<3, uint64_t>(bc, nc, rc);
+      if (xc != xb || cap(nc) != cap(nb) || bc != bb || rc.pos != rb.pos) bad++;
+    }
   }
   return bad;
 }

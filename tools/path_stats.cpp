@@ -28,6 +28,18 @@ struct Rd {
     e2a = t[c2];
     e2b = t[c2 + (1u << cuzfp::kChunkBits)];
   }
+  void chunks_fast(uint32_t g, bool last, uint32_t& e1, uint32_t& e2a, uint32_t& e2b) const {
+    const uint32_t* t = table().e;
+    const uint32_t gm = (g & 1u) ? g : 0u;
+    const uint32_t c2 = (gm >> cuzfp::kChunkBits) & cuzfp::kChunkMask;
+    e1 = t[last ? cuzfp::kLastPosEntry + (g & 1u) : (2u << cuzfp::kChunkBits) | (gm & cuzfp::kChunkMask)];
+    e2a = t[c2];
+    e2b = t[c2 + (1u << cuzfp::kChunkBits)];
+  }
+  uint32_t chunk1_fast(uint32_t g, bool last) const {
+    const uint32_t gm = (g & 1u) ? g : 0u;
+    return table().e[last ? cuzfp::kLastPosEntry + (g & 1u) : (2u << cuzfp::kChunkBits) | (gm & cuzfp::kChunkMask)];
+  }
   uint32_t chunk1(uint32_t g, bool group) const {
     return table().e[group ? (2u << cuzfp::kChunkBits) | (g & cuzfp::kChunkMask) : cuzfp::kNoGroupEntry];
   }
