@@ -216,7 +216,7 @@ def copy(src, dst, stream=None):
     return dst
 
 
-def compress_host(a: np.ndarray, maxbits: int, nstreams: int = 2, out: np.ndarray | None = None):
+def compress_host(a: np.ndarray, maxbits: int, nstreams: int = 4, out: np.ndarray | None = None):
     """Host array -> host stream (uint64 words) through the pinned, overlapped pipeline."""
     a = np.ascontiguousarray(a)
     nx, ny, nz = _extents(a.shape)
@@ -234,7 +234,7 @@ def compress_host(a: np.ndarray, maxbits: int, nstreams: int = 2, out: np.ndarra
     return out
 
 
-def decompress_host(words: np.ndarray, shape, dtype, maxbits: int, nstreams: int = 2,
+def decompress_host(words: np.ndarray, shape, dtype, maxbits: int, nstreams: int = 4,
                     out: np.ndarray | None = None):
     words = np.ascontiguousarray(words)
     if out is None:

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 #include "launch.hpp"
@@ -94,7 +95,11 @@ static uint32_t waves_of(const Geometry& g) { return (g.nblocks + kLanes - 1) / 
 // Pinned (hipHostMalloc / registered) user buffers are DMA'd in place;
 // pageable ones go through a ring of pinned staging buffers.
 
-constexpr size_t kChunkBytes = 32u << 20;
+// 8 MiB chunks on 4 streams: tools/host_sweep.py (profiles/r02_host_sweep.txt),
+// 256^3 f32 rate 8 from pinned buffers: 43-46 GB/s each way against a 52.6 /
+// 55.0 GB/s pinned H2D / D2H link; 32 MiB on 2 streams 43 GB/s; 1 stream
+// 21-43 GB/s; 2-4 MiB chunks 32-47 GB/s, noisier.
+constexpr size_t kChunkBytes = 8u << 20;
 
 // chunk size: kChunkBytes, or CUZFP_HOST_CHUNK_BYTES from the environment
 // (read per call; tests use small chunks to run the multi-chunk paths)
@@ -121,21 +126,70 @@ struct Chunk {
   uint32_t w0, w1;  // wave range for the kernel
 };
 
-struct PipelineRes {
-  std::vector<hipStream_t> st;
-  std::vector<hipEvent_t> ev_in, ev_kernel, ev_done;
-  std::vector<void*> pin_in, pin_out;
-  void* d_data = nullptr;
-  void* d_stream = nullptr;
-  ~PipelineRes() {
-    for (auto s : st) (void)hipStreamDestroy(s);
-    for (auto e : ev_in) (void)hipEventDestroy(e);
-    for (auto e : ev_kernel) (void)hipEventDestroy(e);
-    for (auto e : ev_done) (void)hipEventDestroy(e);
-    for (auto b : pin_in) (void)hipHostFree(b);
-    for (auto b : pin_out) (void)hipHostFree(b);
-    if (d_data) (void)hipFree(d_data);
-    if (d_stream) (void)hipFree(d_stream);
+// The pipeline's device buffers, streams, events and pinned staging ring,
+// kept between calls (per device, one call at a time): allocating and freeing
+// them per call cost about as much as the transfers of a 64 MiB array.
+// Buffers grow to the largest call seen up to kCacheLimit bytes; larger calls
+// use buffers of their own, freed on return.
+constexpr size_t kCacheLimit = 1ull << 30;
+constexpr int kMaxStreams = 8;
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  bool owned_by_call = false;
+  hipError_t get(size_t bytes) {  // at least `bytes`, contents undefined
+    if (bytes <= cap) return hipSuccess;
+    if (p && !owned_by_call) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    const hipError_t e = hipMalloc(&p, std::max<size_t>(bytes, 16));
+    if (e == hipSuccess) cap = bytes;
+    return e;
+  }
+};
+
+struct HostBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t get(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    const hipError_t e = hipHostMalloc(&p, std::max<size_t>(bytes, 16), hipHostMallocDefault);
+    if (e == hipSuccess) cap = bytes;
+    return e;
+  }
+};
+
+struct PipelineCache {
+  int device = -1;
+  DevBuf d_data, d_stream;
+  hipStream_t st[kMaxStreams] = {};
+  hipEvent_t ev_in[kMaxStreams] = {}, ev_kernel[kMaxStreams] = {}, ev_done[kMaxStreams] = {};
+  HostBuf pin_in[kMaxStreams], pin_out[kMaxStreams];
+  int nst = 0;
+};
+
+std::mutex g_pipeline_mu;
+PipelineCache g_pipeline[16];  // by device ordinal; intentionally never freed (process lifetime)
+
+// device buffers for one call: the cache's, or the call's own past kCacheLimit
+struct CallBuf {
+  void* p = nullptr;
+  bool own = false;
+  ~CallBuf() {
+    if (own && p) (void)hipFree(p);
+  }
+  hipError_t get(DevBuf& cached, size_t bytes) {
+    if (bytes <= kCacheLimit) {
+      const hipError_t e = cached.get(bytes);
+      p = cached.p;
+      return e;
+    }
+    own = true;
+    return hipMalloc(&p, bytes);
   }
 };
 }  // namespace
@@ -191,12 +245,17 @@ static int host_pipeline(const Problem& p, bool encode, void* h_data, void* h_st
     chunks.push_back(c);
   }
 
-  const int S = std::max(1, std::min(nstreams, 8));
+  const int S = std::max(1, std::min(nstreams, kMaxStreams));
   const bool data_pinned = is_pinned_host(h_data);
   const bool stream_pinned = is_pinned_host(h_stream);
-  PipelineRes r;
-  CUZFP_HIP_TRY(hipMalloc(&r.d_data, std::max<size_t>(data_bytes, 16)));
-  CUZFP_HIP_TRY(hipMalloc(&r.d_stream, std::max<size_t>(sbytes, 16)));
+  int dev = 0;
+  CUZFP_HIP_TRY(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 16) return CUZFP_ERROR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lock(g_pipeline_mu);
+  PipelineCache& r = g_pipeline[dev];
+  CallBuf bd, bs;
+  CUZFP_HIP_TRY(bd.get(r.d_data, data_bytes));
+  CUZFP_HIP_TRY(bs.get(r.d_stream, sbytes));
   size_t max_in = 0, max_out = 0;
   for (const Chunk& c : chunks) {
     max_in = std::max(max_in, encode ? c.d1 - c.d0 : c.s1 - c.s0);
@@ -204,29 +263,31 @@ static int host_pipeline(const Problem& p, bool encode, void* h_data, void* h_st
   }
   const bool in_pinned = encode ? data_pinned : stream_pinned;
   const bool out_pinned = encode ? stream_pinned : data_pinned;
-  r.st.resize(S);
-  r.ev_in.resize(S);
-  r.ev_kernel.resize(S);
-  r.ev_done.resize(S);
-  for (int i = 0; i < S; i++) {
+  for (int i = r.nst; i < S; i++) {
     CUZFP_HIP_TRY(hipStreamCreateWithFlags(&r.st[i], hipStreamNonBlocking));
     CUZFP_HIP_TRY(hipEventCreateWithFlags(&r.ev_in[i], hipEventDisableTiming));
     CUZFP_HIP_TRY(hipEventCreateWithFlags(&r.ev_kernel[i], hipEventDisableTiming));
     CUZFP_HIP_TRY(hipEventCreateWithFlags(&r.ev_done[i], hipEventDisableTiming));
-    void* b = nullptr;
-    if (!in_pinned) {
-      CUZFP_HIP_TRY(hipHostMalloc(&b, std::max<size_t>(max_in, 16), hipHostMallocDefault));
-      r.pin_in.push_back(b);
-    }
-    if (!out_pinned) {
-      CUZFP_HIP_TRY(hipHostMalloc(&b, std::max<size_t>(max_out, 16), hipHostMallocDefault));
-      r.pin_out.push_back(b);
-    }
+    r.nst = i + 1;
   }
+  for (int i = 0; i < S; i++) {
+    if (!in_pinned) CUZFP_HIP_TRY(r.pin_in[i].get(max_in));
+    if (!out_pinned) CUZFP_HIP_TRY(r.pin_out[i].get(max_out));
+  }
+  // on every return (an error included) nothing of this call is left running
+  // on the cached streams when the next call reuses them (declared after the
+  // call's own buffers, so it runs before they are freed)
+  struct Drain {
+    PipelineCache& r;
+    int S;
+    ~Drain() {
+      for (int i = 0; i < S; i++) (void)hipStreamSynchronize(r.st[i]);
+    }
+  } drain{r, S};
   char* hd = (char*)h_data;
   char* hs = (char*)h_stream;
-  char* dd = (char*)r.d_data;
-  char* ds = (char*)r.d_stream;
+  char* dd = (char*)bd.p;
+  char* ds = (char*)bs.p;
   auto out_range = [&](const Chunk& c, size_t* o0, size_t* o1) {
     *o0 = encode ? c.s0 : c.d0;
     *o1 = encode ? c.s1 : c.d1;
@@ -241,7 +302,7 @@ static int host_pipeline(const Problem& p, bool encode, void* h_data, void* h_st
       if (!out_pinned) {
         size_t o0, o1;
         out_range(chunks[j], &o0, &o1);
-        if (o1 > o0) std::memcpy((encode ? hs : hd) + o0, r.pin_out[sj], o1 - o0);
+        if (o1 > o0) std::memcpy((encode ? hs : hd) + o0, r.pin_out[sj].p, o1 - o0);
       }
     }
     if (i >= n) continue;
@@ -254,8 +315,8 @@ static int host_pipeline(const Problem& p, bool encode, void* h_data, void* h_st
     char* dst = (encode ? dd : ds) + i0;
     if (i1 > i0) {
       if (!in_pinned) {
-        std::memcpy(r.pin_in[s], src, i1 - i0);
-        src = (char*)r.pin_in[s];
+        std::memcpy(r.pin_in[s].p, src, i1 - i0);
+        src = (char*)r.pin_in[s].p;
       }
       CUZFP_HIP_TRY(hipMemcpyAsync(dst, src, i1 - i0, hipMemcpyHostToDevice, st));
     }
@@ -276,7 +337,7 @@ static int host_pipeline(const Problem& p, bool encode, void* h_data, void* h_st
     out_range(c, &o0, &o1);
     if (o1 > o0) {
       char* osrc = (encode ? ds : dd) + o0;
-      char* odst = out_pinned ? (encode ? hs : hd) + o0 : (char*)r.pin_out[s];
+      char* odst = out_pinned ? (encode ? hs : hd) + o0 : (char*)r.pin_out[s].p;
       CUZFP_HIP_TRY(hipMemcpyAsync(odst, osrc, o1 - o0, hipMemcpyDeviceToHost, st));
     }
     CUZFP_HIP_TRY(hipEventRecord(r.ev_done[s], st));

@@ -109,7 +109,7 @@ size_t compress(zfp_stream* stream, zfp_field* field) {
   size_t bytes = 0;
   if (!dev_stream && !dev_field && contiguous(field)) {
     rc = cuzfp_hip_compress_host(field->data, type, nx, ny, nz, stream->maxbits, stream->stream,
-                                 need, &bytes, 2);
+                                 need, &bytes, CUZFP_HOST_STREAMS);
     if (rc) report("compress", rc);
     return rc ? 0 : bytes;
   }
@@ -154,7 +154,7 @@ void decompress(zfp_stream* stream, zfp_field* field) {
   int rc;
   if (!dev_stream && !dev_field && contiguous(field)) {
     rc = cuzfp_hip_decompress_host(stream->stream, need, type, nx, ny, nz, stream->maxbits,
-                                   field->data, 2);
+                                   field->data, CUZFP_HOST_STREAMS);
     if (rc) report("decompress", rc);
     return;
   }

@@ -1313,7 +1313,16 @@ ZFP_HD PW decode_plane_fast(unsigned& bits, unsigned& n, Reader& rd, bool& slow)
   const PW x = (hi & ((PW)ones << nf)) | (~hi & (PW)w);
   n = nf + npos;
   const unsigned adv = nf + used;
+#if defined(CUZFP_EXP_DEC_EXTRA_RT)  // timing experiment: one more dependent LDS round trip a plane
+  {
+    uint32_t a = adv;
+    const uint32_t dummy = rd.window32(rd.pos + adv);
+    asm volatile("; dep %1" : "+v"(a) : "v"(dummy));  // adv waits for the read
+    rd.pos += a;
+  }
+#else
   rd.pos += adv;
+#endif
   bits -= adv;
   return x;
 }

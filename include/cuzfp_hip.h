@@ -63,6 +63,10 @@ extern "C" {
  * 64 KiB. */
 #define CUZFP_MAX_BITS 6144
 
+/* Streams the host-memory pipeline is measured best with (callers' default
+ * `nstreams` for cuzfp_hip_compress_host / decompress_host). */
+#define CUZFP_HOST_STREAMS 4
+
 typedef enum {
   CUZFP_SUCCESS = 0,
   CUZFP_ERROR_INVALID_ARGUMENT = 1, /* bad dims, maxbits or null pointer   */

@@ -18,12 +18,13 @@ p.add_argument("--field", default="polynomial")
 p.add_argument("--dtype", default="float32")
 p.add_argument("--rate", type=float, default=8)
 p.add_argument("--size", type=int, default=256)
+p.add_argument("--dims", type=int, default=3, choices=[1, 2, 3])
 p.add_argument("--reps", type=int, default=5)
 a = p.parse_args()
-shape = (a.size,) * 3
+shape = (a.size,) * a.dims
 arr = polynomial_field(shape, a.dtype) if a.field == "polynomial" else splitmix_uniform(shape, a.dtype)
 x = torch.from_numpy(arr).cuda()
-mb = cz.rate_to_maxbits(a.rate, arr.dtype, 3)
+mb = cz.rate_to_maxbits(a.rate, arr.dtype, a.dims)
 w = cz.encode(x, mb)
 y = cz.decode(w, shape, x.dtype, mb)
 for _ in range(a.reps):
