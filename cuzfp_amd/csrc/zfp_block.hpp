@@ -1401,6 +1401,7 @@ ZFP_HD int decode_half(planes<UInt, DIMS>& P, unsigned& bits, unsigned& n, int c
     if (DIMS == 3 && !any_lane(bits < fast_room<DIMS>::value)) {
       xa = decode_plane_fast_any<DIMS, PW>(bits, n, rd);
       xb = decode_plane_fast_any<DIMS, PW>(bits, n, rd);
+      ZFP_STAMP(4);  // diagnostic builds: the last fast pair's end
     } else {
       xa = decode_plane_any<DIMS, PW>(bits, n, rd);
       xb = decode_plane_any<DIMS, PW>(bits, n, rd);

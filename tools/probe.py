@@ -125,8 +125,8 @@ def analyse(path, name):
           f"{int(np.percentile(rs, 10))} {int(np.median(rs))} {int(np.percentile(rs, 90))} {rs.max()};"
           f"  end ns p10/50/90/max {int(np.percentile(re, 10))} {int(np.median(re))} {int(np.percentile(re, 90))} {re.max()}")
     labels = (["start", "emax(load)", "transform", "transpose", "planes", "-", "end"] if name == "encode"
-              else ["start", "planes", "transpose", "inv-xform", "-", "copy-in", "end"])
-    order = [0, 1, 2, 3, 4, 6] if name == "encode" else [0, 5, 1, 2, 3, 6]
+              else ["start", "planes", "transpose", "inv-xform", "fast pairs", "copy-in", "end"])
+    order = [0, 1, 2, 3, 4, 6] if name == "encode" else [0, 5, 4, 1, 2, 3, 6]
     prev = None
     for k in order:
         col = rel[:, k]
