@@ -159,6 +159,11 @@ template <int DIMS, typename UInt, int... I>
 ZFP_HD void permute_inv(const UInt* u, UInt* q, UInt nb, seq<I...>) {
   ((q[pidx<DIMS, I>::value] = from_negabinary(u[I], nb)), ...);
 }
+// the same for u already XOR-ed with nb (planes::store<true>): one subtraction
+template <int DIMS, typename UInt, int... I>
+ZFP_HD void permute_inv_sub(const UInt* u, UInt* q, UInt nb, seq<I...>) {
+  ((q[pidx<DIMS, I>::value] = u[I] - nb), ...);
+}
 
 // precision() (codec1.c:8-11, codec2.c:131-136, codec3.c:92-97): planes coded
 // for a block with exponent emax in fixed-rate mode (maxprec = type precision,
@@ -276,6 +281,18 @@ ZFP_HD uint32_t nbfi(uint32_t m, uint32_t a, uint32_t b) {
 #endif
 }
 
+// (a & m) | (~b & ~m) in one v_bitop3_b32 (truth table 0xc5: v_bfi's 0xca with b
+// inverted)
+ZFP_HD uint32_t bfi_notb(uint32_t m, uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xc5" : "=v"(r) : "s"(m), "v"(a), "v"(b));
+  return r;
+#else
+  return (a & m) | (~b & ~m);
+#endif
+}
+
 // bytes of {a = bytes 0-3, b = bytes 4-7} picked by sel (v_perm_b32)
 ZFP_HD uint32_t perm_bytes(uint32_t b, uint32_t a, uint32_t sel) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -288,8 +305,13 @@ ZFP_HD uint32_t perm_bytes(uint32_t b, uint32_t a, uint32_t sel) {
 #endif
 }
 
-// INV (last stage only): the odd output words come out inverted
-template <int J, bool INV = false>
+// Output inversion folded into the last stage (J = 1) of a transpose:
+//   kOddWords: the odd output words come out inverted (encoder: the odd planes),
+//   kOddBits:  the odd bit positions of every output word come out inverted
+//              (decoder: the odd planes again, now as bits of coefficients).
+// Either is the "^ 0xaaaa..." of the negabinary conversion, at no cost.
+enum { kInvNone = 0, kOddWords = 1, kOddBits = 2 };
+template <int J, int INV = kInvNone>
 ZFP_HD void transpose_stage(uint32_t* a, int rows) {
   // swap the J x J off-diagonal sub-blocks of every 2J x 2J tile:
   //   lo' = (lo & m) | ((hi << J) & ~m),  hi' = ((lo >> J) & m) | (hi & ~m)
@@ -307,22 +329,28 @@ ZFP_HD void transpose_stage(uint32_t* a, int rows) {
       a[i] = perm_bytes(hi, lo, 0x06020400u);
       a[i + J] = perm_bytes(hi, lo, 0x07030501u);
     } else {
-      a[i] = bfi(m, lo, hi << J);
-      a[i + J] = INV ? nbfi(m, lo >> J, hi) : bfi(m, lo >> J, hi);
+      if constexpr (INV == kOddBits) {  // J = 1, m = 0x5555...: the odd bits come from hi
+        a[i] = bfi_notb(m, lo, hi << J);
+        a[i + J] = bfi_notb(m, lo >> J, hi);
+      } else {
+        a[i] = bfi(m, lo, hi << J);
+        a[i + J] = INV == kOddWords ? nbfi(m, lo >> J, hi) : bfi(m, lo >> J, hi);
+      }
     }
   }
 }
 
-// NEG_ODD: invert the odd output words, i.e. (R even) the odd planes -- the
-// "^ 0xaaaa..." of the negabinary conversion, applied to planes
-template <int R, bool NEG_ODD = false>
+// INV: kOddWords inverts the odd output words, i.e. (R even) the odd planes;
+// kOddBits the odd bits of every output word -- the "^ 0xaaaa..." of the
+// negabinary conversion, applied to planes (encoder) or coefficients (decoder)
+template <int R, int INV = kInvNone>
 ZFP_HD void transpose_tiles(uint32_t* a) {
   // stages J = R/2, ..., 1 spelled out so every index is a compile-time constant
   if constexpr (R >= 32) transpose_stage<16>(a, R);
   if constexpr (R >= 16) transpose_stage<8>(a, R);
   if constexpr (R >= 8) transpose_stage<4>(a, R);
   if constexpr (R >= 4) transpose_stage<2>(a, R);
-  if constexpr (R >= 2) transpose_stage<1, NEG_ODD>(a, R);
+  if constexpr (R >= 2) transpose_stage<1, INV>(a, R);
 }
 
 // Planes of N = 4^DIMS coefficients held as 32-bit words.  For 32-bit
@@ -357,7 +385,7 @@ template <typename UInt, int DIMS> struct planes {
 #pragma unroll
     for (int h = 0; h < H; h++)
 #pragma unroll
-      for (int g = 0; g < G; g++) transpose_tiles<R, NEG_ODD>(&w[h][g * R]);
+      for (int g = 0; g < G; g++) transpose_tiles<R, NEG_ODD ? kOddWords : kInvNone>(&w[h][g * R]);
 #pragma unroll
     for (int h = 0; h < H; h++)
 #pragma unroll
@@ -366,6 +394,9 @@ template <typename UInt, int DIMS> struct planes {
         for (int r = 0; r < R; r++) v[h][g][r] = w[h][g * R + r];
   }
 
+  // NEG_ODD: the coefficients come out as u ^ 0xaaaa... (the first half of
+  // the inverse negabinary conversion)
+  template <bool NEG_ODD = false>
   ZFP_HD void store(UInt* u) const {
     uint32_t w[H][N];
 #pragma unroll
@@ -377,7 +408,7 @@ template <typename UInt, int DIMS> struct planes {
 #pragma unroll
     for (int h = 0; h < H; h++)
 #pragma unroll
-      for (int g = 0; g < G; g++) transpose_tiles<R>(&w[h][g * R]);
+      for (int g = 0; g < G; g++) transpose_tiles<R, NEG_ODD ? kOddBits : kInvNone>(&w[h][g * R]);
 #pragma unroll
     for (int i = 0; i < N; i++) {
       uint64_t x = w[0][i];
@@ -824,11 +855,47 @@ ZFP_HD bool encode_half(const planes<UInt, DIMS>& P, unsigned& n, int cmin, Writ
   return true;
 }
 
+// Planes 31 .. 0 of half H with compile-time plane numbers (every lane of the
+// wave codes all 32 planes while it has budget): each plane word is a fixed
+// register, so there is no VGPR-relative addressing (s_set_gpr_idx_on / off
+// around each read), no readfirstlane of the plane number, and the priority
+// drops sit at fixed trips.
+template <int H, int C, typename UInt, int DIMS, typename Writer>
+ZFP_HD bool encode_half_fixed(const planes<UInt, DIMS>& P, unsigned& n, Writer& wr) {
+  typedef typename plane_word<DIMS>::type PW;
+#if defined(CUZFP_EXP_TRIPS)  // timing experiment: only the first CUZFP_EXP_TRIPS trips (wrong output)
+  if constexpr (C < 31 - 2 * CUZFP_EXP_TRIPS) return true;
+#endif
+  if constexpr (C >= 1) {
+    if (!any_lane(!wr.full())) return false;
+    wr.settle();
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(CUZFP_NO_PRIO)
+    if constexpr (prio_of<Writer>::value) {
+      if constexpr (C == CUZFP_PRIO_T2) __builtin_amdgcn_s_setprio(2);
+      else if constexpr (C == CUZFP_PRIO_T1) __builtin_amdgcn_s_setprio(1);
+      else if constexpr (C == CUZFP_PRIO_T0) __builtin_amdgcn_s_setprio(0);
+    }
+#endif
+    encode_plane_step<DIMS>((PW)P.template get<H>(C), n, wr);
+    encode_plane_step<DIMS>((PW)P.template get<H>(C - 1), n, wr);
+    return encode_half_fixed<H, C - 2>(P, n, wr);
+  }
+  return true;
+}
+
 template <typename UInt, int DIMS, typename Writer>
 ZFP_HD void encode_planes(const planes<UInt, DIMS>& P, unsigned maxprec, Writer& wr) {
   constexpr int PREC = (int)sizeof(UInt) * 8;
   const int kmin = PREC > (int)maxprec ? PREC - (int)maxprec : 0;
   unsigned n = 0;
+#if !defined(CUZFP_ENC_LOOP)  // (CUZFP_ENC_LOOP: the rolled loop below for every block, A/B builds)
+  if constexpr (PREC == 32 && DIMS == 3) {
+    if (!any_lane(kmin != 0)) {  // every lane codes down to plane 0 (normal floats)
+      encode_half_fixed<0, 31>(P, n, wr);
+      return;
+    }
+  }
+#endif
   if constexpr (PREC == 64) {
     if (!encode_half<1>(P, n, kmin > 32 ? kmin - 32 : 0, wr)) return;
   }
@@ -1137,6 +1204,28 @@ ZFP_HD uint32_t drop_if_bit13(uint32_t v, uint32_t e) {
 #endif
 }
 
+// A two-chunk parse that covers position N-1 (npos > q = N-1-n): there the
+// reference reads nothing -- its zero loop stops at N-1 and the one there is
+// implied (decode.c:305-311) -- so the parse past N-1 is not the code.  The
+// code's real end is the start of position N-1's token: in chunk 1 (state 2:
+// its first bit is the leading test) at bit 1 + q + (ones before q), in chunk
+// 2 (chunk 1 read whole, its exit state s1 = a pending group test first) at
+// kChunkBits + s1 + (q - p1) + (ones before q - p1).  Returns that bit count
+// and sets `ones` to the ones below N-1 plus the implied one.
+ZFP_HD uint32_t implied_end(uint32_t e1, uint32_t e2, uint32_t q, uint64_t& ones) {
+  const uint32_t p1 = (e1 >> kPosShift) & 31u;
+  const uint32_t o1 = (e1 >> kOnesShift) & kChunkMask, o2 = (e2 >> kOnesShift) & kChunkMask;
+  uint32_t o;
+  if (p1 > q) {
+    o = 1u + q + (uint32_t)__builtin_popcount(o1 & ((1u << q) - 1u));
+  } else {
+    const uint32_t q2 = q - p1;
+    o = kChunkBits + (e1 >> 31) + q2 + (uint32_t)__builtin_popcount(o2 & ((1u << q2) - 1u));
+  }
+  ones = (ones & ((1ull << q) - 1ull)) | (1ull << q);
+  return o;
+}
+
 template <int DIMS, typename PW, typename Reader>
 ZFP_HD PW decode_plane_lut(unsigned& bits, unsigned& n, Reader& rd, bool& slow) {
   constexpr unsigned N = 1u << (2 * DIMS);
@@ -1177,12 +1266,23 @@ ZFP_HD PW decode_plane_lut(unsigned& bits, unsigned& n, Reader& rd, bool& slow) 
   // and codes the budget cuts short take decode_plane_cont; a code reaching
   // position N-1 the general decoder.
   slow = !(used <= b1 + 1 && npos <= N - 1 - nf);
+  uint64_t ones64 = ones;
+  uint32_t np = npos, take = umin(used, b1);
+  const uint32_t q = N - 1 - nf;
+  if (__builtin_expect(any_lane(npos > q), 0)) {  // the code reaches position N-1 (implied one)
+    if (npos > q) {
+      const uint32_t o = implied_end(e1, e2, q, ones64);
+      slow = o > b1;  // the budget runs out first: the general decoder
+      np = q + 1u;
+      take = o;
+    }
+  }
   // the verbatim bits below m, the new ones at n >= m: one v_bfi_b32 a dword
   // under the mask ~0 << m (m <= N-1)
   const PW hi = (PW)(~0ull << m);
-  const PW x = (hi & ((PW)ones << nf)) | (~hi & (PW)w);
-  n = nf + npos;
-  const unsigned adv = m + umin(used, b1);
+  const PW x = (hi & ((PW)ones64 << nf)) | (~hi & (PW)w);
+  n = nf + np;
+  const unsigned adv = m + take;
   rd.pos += adv;
   bits -= adv;
   return x;
@@ -1307,12 +1407,22 @@ ZFP_HD PW decode_plane_fast(unsigned& bits, unsigned& n, Reader& rd, bool& slow)
   const uint32_t ones = ((e1 >> kOnesShift) & kChunkMask) |
                         (((e2 >> kOnesShift) & kChunkMask) << ((e1 >> kPosShift) & 31u));
   slow = used >= kNotEnded || npos > N - 1 - nf;
+  uint64_t ones64 = ones;
+  uint32_t np = npos, take = used;
+  const uint32_t q = N - 1 - nf;
+  if (__builtin_expect(any_lane(npos > q), 0)) {  // the code reaches position N-1 (implied one)
+    if (npos > q) {
+      take = implied_end(e1, e2, q, ones64);  // within the budget (fast_room)
+      np = q + 1u;
+      slow = false;
+    }
+  }
   // bits >= nf of the plane from the group code, below it verbatim: one
   // v_bfi_b32 a dword under the mask ~0 << nf
   const PW hi = (PW)(~0ull << nf);
-  const PW x = (hi & ((PW)ones << nf)) | (~hi & (PW)w);
-  n = nf + npos;
-  const unsigned adv = nf + used;
+  const PW x = (hi & ((PW)ones64 << nf)) | (~hi & (PW)w);
+  n = nf + np;
+  const unsigned adv = nf + take;
 #if defined(CUZFP_EXP_DEC_EXTRA_RT)  // timing experiment: one more dependent LDS round trip a plane
   {
     uint32_t a = adv;
@@ -1395,6 +1505,9 @@ ZFP_HD int decode_half(planes<UInt, DIMS>& P, unsigned& bits, unsigned& n, int c
   int c = 31;
   for (; c - 1 >= cmin; c -= 2) {
     if (!any_lane(bits != 0)) return c;
+#if defined(CUZFP_EXP_DTRIPS)  // timing experiment: only the first CUZFP_EXP_DTRIPS trips (wrong output)
+    if (c < 31 - 2 * CUZFP_EXP_DTRIPS) return c;
+#endif
     if constexpr (prio_of<Reader>::value)
       progress_priority<CUZFP_DPRIO_T2, CUZFP_DPRIO_T1, CUZFP_DPRIO_T0>(uniform(c));
     PW xa, xb;
@@ -1519,6 +1632,28 @@ template <> struct fp<double> {
 //   plane step and lets a full writer take (and discard) further steps.
 // Reader: peek() returns the next 64 stream bits, skip(n) consumes n <= 64.
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// max |f[i]| over an even number of floats, NaN if any is NaN: v_maximum3_f32
+// with |.| source modifiers, four independent chains
+template <int N>
+__device__ __forceinline__ float absmax_nan(const float* f) {
+  constexpr int C = N >= 16 ? 4 : 1;
+  float m[C];
+#pragma unroll
+  for (int c = 0; c < C; c++) m[c] = 0.0f;
+#pragma unroll
+  for (int i = 0; i < N; i += 2) {
+    float& a = m[(i / 2) % C];
+    asm("v_maximum3_f32 %0, |%1|, |%2|, %0" : "+v"(a) : "v"(f[i]), "v"(f[i + 1]));
+  }
+  if constexpr (C == 4) {
+    asm("v_maximum3_f32 %0, %0, %1, %2" : "+v"(m[0]) : "v"(m[1]), "v"(m[2]));
+    asm("v_maximum3_f32 %0, %0, %1, %1" : "+v"(m[0]) : "v"(m[3]));
+  }
+  return m[0];
+}
+#endif
+
 template <typename Scalar, int DIMS, typename Writer>
 ZFP_HD void encode_block(const Scalar* f, unsigned maxbits, Writer& wr) {
   typedef traits<Scalar> T;
@@ -1530,7 +1665,28 @@ ZFP_HD void encode_block(const Scalar* f, unsigned maxbits, Writer& wr) {
   (void)maxbits;  // the writer owns the budget
   if constexpr (!T::is_int) {
     // encode.c:187-216
+#if defined(__HIP_DEVICE_COMPILE__)
+    // f32 blocks of an even size: max |x| with NaN-propagating v_maximum3_f32,
+    // so that one class test says whether the block is finite (the fast path
+    // below); only a block holding inf or NaN computes the reference's
+    // NaN-ignoring maximum as well.
+    bool finite = false;
+    int emax;
+    if constexpr (sizeof(Scalar) == 4 && N % 2 == 0) {
+      const float mx = absmax_nan<N>((const float*)f);
+      finite = __builtin_isfinite(mx);
+      if (__builtin_expect(finite, 1)) {
+        const uint32_t bm = __builtin_bit_cast(uint32_t, mx);
+        emax = bm ? (int)(bm >> 23) - 126 : -127;
+      } else {
+        emax = fp<Scalar>::template emax<N>((const Scalar*)f);
+      }
+    } else {
+      emax = fp<Scalar>::template emax<N>((const Scalar*)f);
+    }
+#else
     const int emax = fp<Scalar>::template emax<N>((const Scalar*)f);
+#endif
     ZFP_STAMP(1);
     maxprec = precision<DIMS>(emax, T::prec);
     const unsigned e = maxprec ? (unsigned)(emax + T::ebias) : 0u;
@@ -1547,24 +1703,9 @@ ZFP_HD void encode_block(const Scalar* f, unsigned maxbits, Writer& wr) {
 #if defined(__HIP_DEVICE_COMPILE__)
     // Fast path: in a block of finite values with a finite scale, |y| < 2^30
     // (max |x| < 2^emax), so v_cvt_i32_f32's truncation is the x86 cast and
-    // the product pairs go through v_pk_mul_f32.  The block is finite when the
-    // sum of its values is (a NaN or inf makes the sum so; an overflowing sum
-    // of finite values only sends the block down the exact path below).
+    // the product pairs go through v_pk_mul_f32.
     typedef float f2 __attribute__((ext_vector_type(2)));
-    bool fast = false;
-    if constexpr (sizeof(Scalar) == 4 && N % 2 == 0) {
-      // four independent chains: one chain of dependent v_pk_add_f32 stalls a
-      // cycle (an s_nop) per add
-      constexpr int C = N >= 8 ? 4 : 1;
-      f2 acc[C];
-#pragma unroll
-      for (int c = 0; c < C; c++) acc[c] = f2{(float)f[2 * c], (float)f[2 * c + 1]};
-#pragma unroll
-      for (int i = 2 * C; i < N; i += 2) acc[(i / 2) % C] += f2{(float)f[i], (float)f[i + 1]};
-#pragma unroll
-      for (int c = 1; c < C; c++) acc[0] += acc[c];
-      fast = emax >= -97 && __builtin_isfinite(acc[0].x + acc[0].y);
-    }
+    const bool fast = finite && emax >= -97;
     if constexpr (sizeof(Scalar) == 4 && N % 2 == 0) {
       if (fast) {
         const f2 ss = {(float)s, (float)s};
@@ -1688,12 +1829,16 @@ ZFP_HD bool decode_block(Scalar* f, unsigned maxbits, Reader& rd) {
   if constexpr (prio_of<Reader>::value) __builtin_amdgcn_s_setprio(CUZFP_DPRIO_AFTER);  // see progress_priority
 #endif
   ZFP_STAMP(1);
-  P.store(u);
+  P.template store<true>(u);  // u ^ NB
   ZFP_STAMP(2);
 #endif
   UInt q[N];
   constexpr UInt NB = nbmask<UInt>::value;
+#if defined(CUZFP_PROBE) && (CUZFP_PROBE == 1 || CUZFP_PROBE == 2)
   permute_inv<DIMS>(u, q, NB, make_seq<N>());
+#else
+  permute_inv_sub<DIMS>(u, q, NB, make_seq<N>());  // (u ^ NB) - NB
+#endif
   inv_xform<DIMS>(q);
   ZFP_STAMP(3);
   if constexpr (!T::is_int) {

@@ -102,6 +102,10 @@ int main(int argc, char** argv) {
     }
     sum_wave_steps += wsteps;
     wave_steps_hist[wsteps]++;
+    if (getenv("WAVE_DUMP")) {  // per-wave plane steps, one line per wave (load-balance studies)
+      static FILE* wf = fopen(getenv("WAVE_DUMP"), "w");
+      fprintf(wf, "%d\n", wsteps);
+    }
     for (int k = 0; k < wsteps; k++) {
       bool all0 = true, anyw = false, allf = true, allfit = true;
       unsigned gmax = 0;
