@@ -61,9 +61,14 @@ namespace cuzfp {
 // each decode workgroup copies them to LDS.
 __device__ const ChunkLut g_chunk_lut = make_chunk_lut();
 constexpr size_t kChunkLutBytes = sizeof(ChunkLut);
-// ... and the plane coder's spread table (each encode workgroup copies it)
-__device__ const SpreadLut g_spread_lut = make_spread_lut();
-constexpr size_t kSpreadLutBytes = sizeof(SpreadLut);
+// ... and the plane coder's spread tables (2 KiB): a static LDS array at
+// address 0, so a lookup is one ds_read_b32 at (byte << 2) with the table in
+// the offset field.  Every wave of a workgroup writes the whole table itself
+// (the same values to the same addresses) and waits only for its own writes,
+// so the waves need no barrier.
+__device__ const SpreadTab g_spread_tab = make_spread_tab();
+constexpr size_t kSpreadTabBytes = sizeof(SpreadTab);
+typedef __attribute__((address_space(3))) const uint32_t lds_spread;
 
 // ---------------------------------------------------------------------------
 // LDS bit writers / reader (one lane, one block)
@@ -81,20 +86,29 @@ template <bool PRIO = true>
 struct LdsOrWriter {
   static constexpr bool kPrio = PRIO;  // progress_priority schedule (zfp_block.hpp)
   uint64_t* p;          // the lane's column: word j at p[64 j], W + kSlackWords words, zeroed
-  const uint32_t* lut;  // the workgroup's spread table
+  lds_spread* lut;      // the workgroup's spread tables
   uint32_t pos, lim;    // bits produced; 64 * W
 #if defined(CUZFP_EXP_NOPUT)
   uint64_t sink = 0;
 #endif
   __device__ __forceinline__ bool full() const { return pos >= lim; }
   __device__ __forceinline__ void put(uint64_t v, unsigned n) {  // v < 2^n
-    const uint32_t w = pos >> 6, sh = pos & 63;
+    const uint32_t w = pos >> 6;
     uint64_t* q = p + w * 64;
-    atomicOr((unsigned long long*)&q[0], (unsigned long long)(v << sh));
-    atomicOr((unsigned long long*)&q[64], (unsigned long long)((v >> 1) >> (63 - sh)));
+    // the shifts use the low 6 bits of their counts: pos & 63 and
+    // 63 - (pos & 63) = (pos ^ 63) & 63 (one full-rate XOR)
+    uint64_t lo, hi;
+    asm("v_lshlrev_b64 %0, %1, %2" : "=v"(lo) : "v"(pos), "v"(v));
+    asm("v_lshrrev_b64 %0, 1, %1" : "=v"(hi) : "v"(v));
+    asm("v_lshrrev_b64 %0, %1, %0" : "+v"(hi) : "v"(pos ^ 63u));
+    atomicOr((unsigned long long*)&q[0], (unsigned long long)lo);
+    atomicOr((unsigned long long*)&q[64], (unsigned long long)hi);
     pos += n;
   }
-  __device__ __forceinline__ uint32_t spread(uint32_t b) const { return lut[b]; }
+  // o: byte offset of the entry (byte_off8)
+  __device__ __forceinline__ uint32_t sp0(uint32_t o) const { return *(lds_spread*)((uintptr_t)lut + o); }
+  __device__ __forceinline__ uint32_t sp1(uint32_t o) const { return *(lds_spread*)((uintptr_t)(lut + 256) + o); }
+  __device__ __forceinline__ uint32_t spread(uint32_t b) const { return lut[256 + b] >> 1; }
   __device__ __forceinline__ void zero_bit() { pos++; }
 #if defined(CUZFP_EXP_NOPUT)
   __device__ __forceinline__ void finish() { p[0] ^= sink; }
@@ -113,13 +127,15 @@ template <bool PRIO = true>
 struct LdsBitWriter {
   static constexpr bool kPrio = PRIO;
   uint64_t* lds;
-  const uint32_t* lut;     // the workgroup's spread table
+  lds_spread* lut;         // the workgroup's spread tables
   uint32_t pos, end, cnt;  // pos: stream offset of acc's bit 0
   uint64_t acc;
 #if defined(CUZFP_EXP_NOPUT)
   uint64_t sink = 0;
 #endif
-  __device__ __forceinline__ uint32_t spread(uint32_t b) const { return lut[b]; }
+  __device__ __forceinline__ uint32_t sp0(uint32_t o) const { return *(lds_spread*)((uintptr_t)lut + o); }
+  __device__ __forceinline__ uint32_t sp1(uint32_t o) const { return *(lds_spread*)((uintptr_t)(lut + 256) + o); }
+  __device__ __forceinline__ uint32_t spread(uint32_t b) const { return lut[256 + b] >> 1; }
   __device__ __forceinline__ bool full() const { return pos + cnt >= end; }
   __device__ __forceinline__ void emit(uint64_t v) {
     if (pos >= end) return;  // bits past maxbits are dropped
@@ -506,25 +522,29 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS, t
                                                                       Geometry g,
                                                                       uint64_t* __restrict__ stream) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds_all[];
+  __shared__ __attribute__((aligned(16))) uint32_t stab[512];  // LDS address 0 (static)
   constexpr int N = 1 << (2 * DIMS);
   const uint32_t wig = threadIdx.x >> 6;  // wave in workgroup
   const uint32_t wave = g.wave0 + blockIdx.x * (blockDim.x >> 6) + wig;
-  if (wave >= g.wave_end) return;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t b = wave * kLanes + lane;
+  const bool live_wave = wave < g.wave_end;
   uint64_t* lds = lds_all + (size_t)wig * g.lds_words;
-  // the plane coder's spread table, one copy per wave (after the group's
-  // stream images): its load is issued first so that storing it waits only
+  if (!live_wave) return;
+  // the plane coder's spread tables, written whole by every wave (see
+  // g_spread_tab): their load is issued first so that storing them waits only
   // for it, not for the block's gathers
-  const uint4 spread16 = ((const uint4*)g_spread_lut.e)[lane];
+  constexpr uint32_t kTabPieces = kSpreadTabBytes / 16;  // two 16-byte pieces a lane
+  uint4 tab16[kTabPieces / kLanes];
+#pragma unroll
+  for (uint32_t i = 0; i < kTabPieces / kLanes; i++) tab16[i] = ((const uint4*)g_spread_tab.e)[lane + i * kLanes];
   if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);  // lowered through the plane loop (progress_priority)
-  uint32_t* lut = (uint32_t*)(lds_all + (size_t)(blockDim.x >> 6) * g.lds_words) + wig * 256;
+  lds_spread* lut = (lds_spread*)stab;
   ZFP_STAMP_HWID();
   ZFP_STAMP_REAL(8);
   ZFP_STAMP(0);
   if constexpr (!ALIGNED) {
     for (uint32_t j = lane; j < g.maxbits + 2; j += kLanes) lds[j] = 0;
-    wave_lds_sync();
   }
   // ALIGNED: the wave's image is lane-interleaved, word j of lane l's block at
   // lds[64 j + l] (conflict-free ds_or_b64 whatever each lane's bit position),
@@ -536,16 +556,17 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS, t
 #else
   if (b < g.nblocks) gather<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
 #endif
-  ((uint4*)lut)[lane] = spread16;  // every lane: the table is the wave's
+#pragma unroll
+  for (uint32_t i = 0; i < kTabPieces / kLanes; i++) ((uint4*)stab)[lane + i * kLanes] = tab16[i];
   if (b < g.nblocks) {
     if constexpr (ALIGNED) {
       uint64_t* mine = lds + lane;
       for (uint32_t j = 0; j < W + kSlackWords; j++) mine[j * 64] = 0;  // own column
-      wave_lds_sync();  // the wave's table
+      wave_lds_sync();  // the tables
       LdsOrWriter<PRIO> wr{mine, lut, 0, 64 * W};
       encode_block<Scalar, DIMS>(f, g.maxbits, wr);
     } else {
-      wave_lds_sync();  // the wave's table
+      wave_lds_sync();  // the tables and the zeroed image
       LdsBitWriter<PRIO> wr{lds, lut, lane * g.maxbits, (lane + 1) * g.maxbits, 0, 0};
       encode_block<Scalar, DIMS>(f, g.maxbits, wr);
     }
@@ -765,11 +786,12 @@ int launch_encode_t(const void* data, const Geometry& g, bool fast, uint64_t* st
   gg.lds_words = g.maxbits + kLanes * kSlackWords;  // + per-lane slack
   // the word-aligned writer pads each lane with slack words; very large maxbits
   // (whose padded image would pass 64 KiB of LDS) take the general writer
-  const bool aligned = (g.maxbits & 63) == 0 && gg.lds_words * 8 + kSpreadLutBytes <= 65536;
+  const bool aligned = (g.maxbits & 63) == 0 && gg.lds_words * 8 + kSpreadTabBytes <= 65536;
   if (!aligned) gg.lds_words = g.maxbits + 2;
-  const uint32_t wpg = waves_per_group(gg.lds_words + kSpreadLutBytes / 8);
+  // (the spread tables are the kernel's static LDS, kSpreadTabBytes a workgroup)
+  const uint32_t wpg = waves_per_group(gg.lds_words, kSpreadTabBytes);
   const dim3 grid((nwaves + wpg - 1) / wpg), block(kLanes * wpg);
-  const size_t lds = (size_t)wpg * (gg.lds_words * 8 + kSpreadLutBytes);
+  const size_t lds = (size_t)wpg * gg.lds_words * 8;
   const Scalar* d = (const Scalar*)data;
   if (fast && aligned && !use_priority(nwaves, occupancy<Scalar, DIMS, true>::value, 1))
     hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, true, true, false>), grid, block, lds, st, d, gg, stream);

@@ -455,7 +455,7 @@ template <typename UInt, int DIMS> struct planes {
 // most significant first: the first n bits verbatim (coefficients already
 // significant), then group tests: "1" + the bits up to and including the next
 // one bit (the one at position N-1 is implied), until a "0" test or the end of
-// the plane.  Each group is emitted with one writer call.
+// the plane.
 
 // Plane word type: 64 coefficients need 64 bits, 16 or 4 fit in 32.
 template <int DIMS> struct plane_word { typedef uint32_t type; };
@@ -480,62 +480,6 @@ ZFP_HD unsigned ctz64_or_64(uint64_t x) {
   const unsigned zh = hi ? 32u + (unsigned)__builtin_ctz(hi) : 64u;
   return zl < zh ? zl : zh;
 #endif
-}
-
-// Encoder plane step.  With n coefficients already significant the plane's
-// code is: its first n bits verbatim, then for every further one bit at
-// position p a group "1" + the zeros before p + that one (implied, so omitted,
-// when p = N-1), then a closing "0" group test if positions remain.  The
-// common case is two writer calls and no branch on the data: the verbatim bits,
-// then the whole group code G built with one shift per new one.  Writers drop
-// bits past maxbits, so a plane that crosses the budget needs no clipping here
-// and the stream is exactly the reference's budget-truncated prefix; the plane
-// loop stops once the writer reports full().
-template <int DIMS, typename PW, typename Writer>
-ZFP_HD void encode_plane(PW x, unsigned& n, Writer& wr) {
-  constexpr unsigned N = 1u << (2 * DIMS);
-  wr.put(x & (PW)lowmask(n), n);  // verbatim part (nothing when n = 0)
-  // new ones, in the frame of the first not-yet-significant coefficient
-  const PW r = n < N ? (PW)(x >> (n & (8 * sizeof(PW) - 1))) : (PW)0;
-  // With t new ones at relative positions p_0 < ... < p_{t-1} the group code
-  // is  1 (z_0 zeros) 1 1 (z_1 zeros) 1 1 ... (z_{t-1} zeros) 1 0,  i.e. "1"
-  // followed by the segment up to p_{t-1} with every one doubled, the last
-  // one's partner being the closing "0" -- or, when the last one sits at
-  // position N-1, both its bit and the closing test omitted.  The j-th one
-  // therefore lands at bit p_j + j + 1 (and its partner at + 2).  No new ones:
-  // the single group test "0" (none at all once n = N).
-  const unsigned t = (unsigned)(sizeof(PW) == 8 ? __builtin_popcountll((uint64_t)r) : __builtin_popcount((uint32_t)r));
-  const unsigned pt = r ? (unsigned)(8 * sizeof(PW) - 1) - (unsigned)(sizeof(PW) == 8 ? __builtin_clzll((uint64_t)r) : __builtin_clz((uint32_t)r)) : 0u;
-  const unsigned qmax = pt + t - 1;  // G position of the last one, minus 1
-  if (__builtin_expect(!r || qmax <= 61, 1)) {
-    uint64_t F = 0;
-    PW rr = r;
-    unsigned j = 0;
-    while (rr) {
-      const PW low = rr & (PW)(0 - rr);
-      F |= (uint64_t)low << j;
-      rr ^= low;
-      j++;
-    }
-    const bool last_n = pt + n == N - 1;
-    const unsigned L = r ? qmax + (last_n ? 1u : 3u) : (n < N ? 1u : 0u);
-    const uint64_t G = r ? (1ull | (F << 1) | (F << 2)) & lowmask(last_n ? L : L - 1) : 0ull;
-    wr.put(G, L);
-    n += r ? pt + 1 : 0u;
-  } else {
-    // dense plane (many ones early in a wide block): one put per group
-    PW rest = r;
-    unsigned base = n;
-    while (rest && !wr.full()) {
-      const unsigned p = ctz(rest);
-      const bool last = base + p == N - 1;
-      const unsigned z = p - (n - base);
-      wr.put(last ? 1ull : (1ull | (2ull << z)), z + (last ? 1u : 2u));
-      n = base + p + 1;
-      rest &= rest - 1;
-    }
-    if (n < N && !wr.full()) wr.zero_bit();
-  }
 }
 
 // Plane loop, most significant plane first (encode.c:133-150).  The plane
@@ -648,12 +592,33 @@ constexpr SpreadLut make_spread_lut() {
   return t;
 }
 
-// bit length of x < 2^24 (0 for 0): the exponent of (float)x, which frexp
-// gives as x in [2^(e-1), 2^e) -- two instructions, no zero test
+// The one-put coder's tables, one dword an entry: table 0 (r's low byte)
+// entry b = (spread(b) << 1 | 1) << 5 | (popcount(b) + 8) -- the group code's
+// leading "1" in place, and in the low 5 bits the shift that places the high
+// byte's part; table 1 (r's high byte) entry b = spread(b) << 1.  The group
+// code of r < 2^16 is then e1 << e0[4:0] | e0 >> 5: one v_lshl_or_b32 (whose
+// shift count is the low 5 bits of its operand) and one shift.
+struct SpreadTab {
+  uint32_t e[512];
+};
+constexpr SpreadTab make_spread_tab() {
+  SpreadTab t{};
+  for (uint32_t b = 0; b < 256; b++) {
+    uint32_t pop = 0;
+    for (int i = 0; i < 8; i++) pop += (b >> i) & 1u;
+    t.e[b] = (((spread_entry(b) << 1) | 1u) << 5) | (pop + 8u);
+    t.e[256 + b] = spread_entry(b) << 1;
+  }
+  return t;
+}
+
+// bit length of x (0 for 0): 32 - clz(x), where v_ffbh_u32 gives ~0 for 0 and
+// the saturating (clamp) subtraction turns 32 - ~0 into 0 -- one half-rate and
+// one full-rate instruction, no zero test
 ZFP_HD uint32_t bitlen16(uint32_t x) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  uint32_t e;  // (the compiler's own u32 -> f32 form is the exact 64-bit one: 8 instructions)
-  asm("v_cvt_f32_u32 %0, %1\n\tv_frexp_exp_i32_f32 %0, %0" : "=&v"(e) : "v"(x));
+  uint32_t e;
+  asm("v_ffbh_u32 %0, %1\n\tv_sub_u32_e64 %0, 32, %0 clamp" : "=&v"(e) : "v"(x));
   return e;
 #else
   return x ? 32u - (uint32_t)__builtin_clz(x) : 0u;
@@ -672,50 +637,22 @@ ZFP_HD uint64_t shl64(uint64_t v, uint32_t s) {
 #endif
 }
 
-template <int DIMS, bool CHECK = true, typename PW, typename Writer>
-ZFP_HD bool encode_plane_lut(PW x, unsigned& n, Writer& wr) {
-  constexpr unsigned N = 1u << (2 * DIMS);
-  const uint64_t xx = (uint64_t)x;
-  const uint64_t r = n < N ? xx >> (n & 63) : 0ull;
-  if (CHECK && (r >> 16)) return false;
-  const uint64_t v = xx ^ shl64(r, n);  // the verbatim bits x & lowmask(n)
-  const uint32_t rl = (uint32_t)r, b0 = rl & 0xffu, b1 = rl >> 8;
-  const uint32_t p0 = (uint32_t)__builtin_popcount(b0);
-  // r, ones doubled (1D: r has at most 4 bits, one table read)
-  const uint32_t t = N <= 8 ? p0 : p0 + (uint32_t)__builtin_popcount(b1);
-  const uint32_t E = N <= 8 ? wr.spread(b0) : wr.spread(b0) | (wr.spread(b1) << (8 + p0));
-  const uint32_t nz = rl ? 1u : 0u;                                   // any new ones
-  const uint32_t bl = bitlen16(rl);                                   // positions covered
-  const uint32_t L = bl + t;                                          // bits of E
-  const uint32_t imp = n + bl == N ? nz : 0u;                         // top one at N-1: implied
-  // branch-free: "1" + E with the top one's test flipped to the closing "0"
-  // (imp: that one and its test dropped instead); no new ones: G = 0 and the
-  // single "0" test (none once n = N)
-  const uint64_t G = (((uint64_t)E << 1) | nz) ^ ((uint64_t)(nz | (imp << 1)) << ((L - imp) & 63));
-  const uint32_t glen = L + (n < N ? 1u : 0u) - 2u * imp;
-  wr.put(v, n);
-  wr.put(G, glen);
-  n += bl;
-  return true;
-}
-
-// general plane step: the two-put table coder, or the exact group coder for
-// a dense plane
-template <int DIMS, typename PW, typename Writer>
-ZFP_HD void encode_plane_any(PW x, unsigned& n, Writer& wr) {
-  // one wave-uniform test: the per-lane branch around the table coder costs
-  // ~6 exec-mask instructions a plane even when no lane takes it
-  constexpr unsigned N = 1u << (2 * DIMS);
-  if constexpr (N <= 16) {  // r has at most 16 bits: never dense
-    encode_plane_lut<DIMS, false>(x, n, wr);
-    return;
-  }
-  const uint64_t r = n < N ? (uint64_t)x >> (n & 63) : 0ull;
-  if (__builtin_expect(any_lane((r >> 16) != 0), 0)) {
-    if (!encode_plane_lut<DIMS>(x, n, wr)) encode_plane<DIMS>(x, n, wr);
-  } else {
-    encode_plane_lut<DIMS, false>(x, n, wr);
-  }
+// byte I of v times 4: the byte offset of its entry in a table of dwords.
+// Two full-rate instructions (shift by an immediate, AND with a literal); the
+// compiler's SDWA form takes the shift count from a VGPR, which issues at half
+// rate (tools/ubench/opcost.hip).
+template <int I>
+ZFP_HD uint32_t byte_off4(uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t r;
+  if constexpr (I == 0)
+    asm("v_lshlrev_b32 %0, 2, %1\n\tv_and_b32 %0, 0x3fc, %0" : "=&v"(r) : "v"(v));
+  else
+    asm("v_lshrrev_b32 %0, %2, %1\n\tv_and_b32 %0, 0x3fc, %0" : "=&v"(r) : "v"(v), "i"(8 * I - 2));
+  return r;
+#else
+  return ((v >> (8 * I)) & 0xffu) << 2;
+#endif
 }
 
 // v_bfe_u32(v, 0, w): the low w bits of v, w = 0 .. 31
@@ -747,13 +684,15 @@ ZFP_HD void encode_plane_one_put(PW x, unsigned nf, uint32_t rl, uint32_t bl, ui
   const uint32_t imp = nn >> (2 * DIMS);  // r's top one at N-1
   const uint32_t width = L - imp;
   const uint32_t len = nf + width + 1u - imp;
-  const uint32_t b0 = rl & 0xffu;
-  const uint32_t E = N <= 4 ? wr.spread(b0)
-                            : wr.spread(b0) | (wr.spread(rl >> 8) << (uint32_t)(__builtin_popcount(b0) + 8));
-  const uint32_t g = low_bits((E << 1) | 1u, width);
+  // "1" + r with every one doubled: one table entry a byte of r (3D: r < 2^15,
+  // 2D: r < 2^16; where r's top bits move past bit 31 they lie past width)
+  const uint32_t e0 = wr.sp0(byte_off4<0>(rl));
+  uint32_t G = e0 >> 5;
+  if constexpr (N > 4) G |= wr.sp1(byte_off4<1>(rl)) << (e0 & 31u);
+  const uint32_t g = low_bits(G, width);
   const uint64_t code = (uint64_t)x ^ ((uint64_t)(rl ^ g) << nf);
   wr.put(code, len);
-  n = nn < N - 1 ? nn : N - 1;
+  n = nn - imp;  // min(nn, N-1)
 }
 
 // r with every one doubled, for a 32-bit r: four byte lookups placed at
@@ -782,7 +721,7 @@ ZFP_HD uint32_t bitlen32(uint32_t x) { return x ? 32u - (uint32_t)__builtin_clz(
 template <typename Writer>
 ZFP_HD void encode_plane_wide(uint64_t x, unsigned& n, Writer& wr) {
   wr.settle();
-  const unsigned nf = n < 63u ? n : 63u;
+  const unsigned nf = n;  // <= 63
   const uint64_t r = x >> nf;
   const uint32_t lo = (uint32_t)r, hi = (uint32_t)(r >> 32);
   const uint32_t blh = bitlen32(hi);
@@ -806,16 +745,16 @@ ZFP_HD void encode_plane_wide(uint64_t x, unsigned& n, Writer& wr) {
   // drop the top one's partner (imp: the top one too); ltop >= 2 when r != 0
   const uint64_t cut = nz ? (uint64_t)(2u + imp) << ((ltop - 2u) & 63) : 0ull;
   wr.put(top & ~cut, ltop - 2u * imp);  // + the closing "0" (unless imp)
-  n = nn < 63u ? nn : 63u;
+  n = nn - imp;  // min(nn, 63)
 }
 
 template <int DIMS, typename PW, typename Writer>
 ZFP_HD void encode_plane_step(PW x, unsigned& n, Writer& wr) {
   constexpr unsigned N = 1u << (2 * DIMS);
-  const unsigned nf = n < N - 1 ? n : N - 1;
+  const unsigned nf = n;  // both steps keep n <= N-1
   const uint64_t r = (uint64_t)x >> nf;
   const uint32_t rl = (uint32_t)r;
-  const uint32_t bl = bitlen16(rl);                           // exact for r < 2^24
+  const uint32_t bl = bitlen16(rl);
   const uint32_t L = (uint32_t)__builtin_popcount(rl) + bl;  // v_bcnt_u32_b32(rl, bl)
   if constexpr (N <= 16) {
     // r has at most 16 bits and the code at most 48: always one put

@@ -44,6 +44,12 @@ struct HostWriter {
     static const cuzfp::SpreadLut t = cuzfp::make_spread_lut();
     return t.e[b];
   }
+  uint32_t sp0(uint32_t o) const { return tab().e[o >> 2]; }  // o: byte offset
+  uint32_t sp1(uint32_t o) const { return tab().e[256 + (o >> 2)]; }
+  static const cuzfp::SpreadTab& tab() {
+    static const cuzfp::SpreadTab t = cuzfp::make_spread_tab();
+    return t;
+  }
 };
 
 struct HostReader {
