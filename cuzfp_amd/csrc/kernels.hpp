@@ -183,7 +183,7 @@ template <bool PRIO = true>
 struct LdsReader {
   static constexpr bool kPrio = PRIO;
   const uint32_t* lds32;
-  const uint32_t* lut32;  // the workgroup's copy of the chunk tables
+  const uint32_t* lut32;  // the workgroup's copy of the chunk tables (static LDS)
   uint32_t pos;
   uint32_t x0, x1, x2, x3, x4;
   // byte address of the row holding bit p: lds32 + 256 * (p >> 5), in two
@@ -212,51 +212,54 @@ struct LdsReader {
         ((uint64_t)__builtin_amdgcn_alignbit(a2, a1, pos) << 32);
     g = __builtin_amdgcn_alignbit(b1, b0, q);
   }
-  // table decoder: entry (2, g's chunk 1) -- or the no-group entry -- and
-  // entries (0, chunk 2), (1, chunk 2); addresses in two instructions each
-  // (the compiler's forms take three)
-  __device__ __forceinline__ void chunks(uint32_t g, bool group, uint32_t& e1, uint32_t& e2a,
-                                         uint32_t& e2b) const {
+  // The chunk tables are the kernel's static LDS (address 0), so an entry's
+  // byte offset goes straight into ds_read's address with the state in the
+  // offset field.  (The plane loops are bound by the count of VALU
+  // instructions -- SQ_ACTIVE_INST_VALU is one quad-cycle per instruction,
+  // with two issued together in about a tenth of them, SQ_ACTIVE_INST_VALU2 --
+  // so the offsets are built with the fewest instructions, three-input ones
+  // included.)
+  __device__ __forceinline__ uint32_t tab(uint32_t byte_off) const {
+    return *(lds_u32*)((uintptr_t)(lds_u32*)lut32 + byte_off);
+  }
+  // g with every bit cleared unless its leading group test (bit 0) is 1: a
+  // lane whose test reads "0" (no new ones: about half the lane-steps) looks
+  // up entry 0 for both chunks -- the same "0" entry as any even chunk, and a
+  // chunk 2 that is dropped anyway -- so those lanes' reads are broadcasts
+  // instead of bank conflicts (random entries made 51 % of the decoder's LDS
+  // cycles conflict cycles, SQ_LDS_BANK_CONFLICT)
+  static __device__ __forceinline__ uint32_t lead_masked(uint32_t g) {
+    uint32_t t;
+    asm("v_bfe_i32 %0, %1, 0, 1" : "=v"(t) : "v"(g));
+    return g & t;
+  }
+  // byte offsets of chunk 1 (bits 0-9) and chunk 2 (bits 10-19) in a state's table
+  static __device__ __forceinline__ uint32_t off1(uint32_t gm) {
+    uint32_t a;
+    asm("v_lshlrev_b32 %0, 2, %1\n\tv_and_b32 %0, 0xffc, %0" : "=&v"(a) : "v"(gm));
+    return a;
+  }
+  static __device__ __forceinline__ uint32_t off2(uint32_t gm) {
+    uint32_t a;
+    asm("v_lshrrev_b32 %0, 8, %1\n\tv_and_b32 %0, 0xffc, %0" : "=&v"(a) : "v"(gm));
+    return a;
+  }
+  static constexpr uint32_t kStateBytes = 4u << kChunkBits;  // one state's table
+  // the table steps' lookups: entry (2, g's chunk 1) and entries (0, chunk 2),
+  // (1, chunk 2).  (With n = N-1 the group part is the last position's bit
+  // alone; the parse then runs past position N-1, which the steps' implied-one
+  // rule resolves.)
+  __device__ __forceinline__ void chunks_fast(uint32_t g, uint32_t& e1, uint32_t& e2a, uint32_t& e2b) const {
 #if defined(CUZFP_EXP_DEC_NOLUT)  // timing experiment: no table reads (short ended codes), wrong output
     e1 = pack_entry(g & 0x3ffu, ((g >> 10) & 7u) + 1u, ((g >> 13) & 7u) + 1u, 0);
     e2a = e2b = 0;
-    (void)group;
     return;
 #endif
-    const uint32_t base = (uint32_t)(uintptr_t)(lds_u32*)lut32;
-    // A lane whose leading group test reads "0" (no new ones: about half the
-    // lane-steps) looks up entry 0 for both chunks -- the same "0" entry as
-    // any even chunk, and a chunk 2 that is dropped anyway -- so those lanes'
-    // reads are broadcasts instead of bank conflicts (random entries made 51 %
-    // of the decoder's LDS cycles conflict cycles, SQ_LDS_BANK_CONFLICT).
-    uint32_t t;
-    asm("v_bfe_i32 %0, %1, 0, 1" : "=v"(t) : "v"(g));  // -(leading test bit)
-    const uint32_t gm = g & t;
-    const uint32_t c1 = group ? (gm & kChunkMask) : kNoGroupEntry - (2u << kChunkBits);
-    uint32_t a1, c2, a2;
-    asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a1) : "v"(c1), "s"(base));
-    asm("v_bfe_u32 %0, %1, %2, %2" : "=v"(c2) : "v"(gm), "i"(kChunkBits));
-    asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a2) : "v"(c2), "s"(base));
-    e1 = ((lds_u32*)(uintptr_t)a1)[2u << kChunkBits];
-    e2a = ((lds_u32*)(uintptr_t)a2)[0];
-    e2b = ((lds_u32*)(uintptr_t)a2)[1u << kChunkBits];
-  }
-  // the fast step's lookups: as chunks(), with n = N-1 (last) taking the two
-  // last-position entries by the group test bit instead of a chunk
-  __device__ __forceinline__ void chunks_fast(uint32_t g, bool last, uint32_t& e1, uint32_t& e2a,
-                                              uint32_t& e2b) const {
-    const uint32_t base = (uint32_t)(uintptr_t)(lds_u32*)lut32;
-    uint32_t t;
-    asm("v_bfe_i32 %0, %1, 0, 1" : "=v"(t) : "v"(g));  // "0" leading test: entry 0 (see chunks)
-    const uint32_t gm = g & t;
-    const uint32_t c1 = last ? ((kLastPosEntry - (2u << kChunkBits)) | (g & 1u)) : (gm & kChunkMask);
-    uint32_t a1, c2, a2;
-    asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a1) : "v"(c1), "s"(base));
-    asm("v_bfe_u32 %0, %1, %2, %2" : "=v"(c2) : "v"(gm), "i"(kChunkBits));
-    asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a2) : "v"(c2), "s"(base));
-    e1 = ((lds_u32*)(uintptr_t)a1)[2u << kChunkBits];
-    e2a = ((lds_u32*)(uintptr_t)a2)[0];
-    e2b = ((lds_u32*)(uintptr_t)a2)[1u << kChunkBits];
+    const uint32_t gm = lead_masked(g);
+    const uint32_t a2 = off2(gm);
+    e1 = tab(2 * kStateBytes + off1(gm));
+    e2a = tab(a2);
+    e2b = tab(kStateBytes + a2);
   }
   // continuation pairs (dense planes): 32 stream bits at bit q of the block,
   // chunk A in state st (0/1), chunk B in states 0 and 1
@@ -266,33 +269,13 @@ struct LdsReader {
   }
   __device__ __forceinline__ void chunks_st(uint32_t g, uint32_t st, uint32_t& eA, uint32_t& eBa,
                                             uint32_t& eBb) const {
-    const uint32_t base = (uint32_t)(uintptr_t)(lds_u32*)lut32;
-    const uint32_t cA = (g & kChunkMask) | (st << kChunkBits);
-    uint32_t aA, c2, a2;
-    asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(aA) : "v"(cA), "s"(base));
-    asm("v_bfe_u32 %0, %1, %2, %2" : "=v"(c2) : "v"(g), "i"(kChunkBits));
-    asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a2) : "v"(c2), "s"(base));
-    eA = ((lds_u32*)(uintptr_t)aA)[0];
-    eBa = ((lds_u32*)(uintptr_t)a2)[0];
-    eBb = ((lds_u32*)(uintptr_t)a2)[1u << kChunkBits];
+    const uint32_t a2 = off2(g);
+    eA = tab((st << 12) + off1(g));
+    eBa = tab(a2);
+    eBb = tab(kStateBytes + a2);
   }
-  __device__ __forceinline__ uint32_t chunk1_fast(uint32_t g, bool last) const {
-    const uint32_t base = (uint32_t)(uintptr_t)(lds_u32*)lut32;
-    uint32_t t;
-    asm("v_bfe_i32 %0, %1, 0, 1" : "=v"(t) : "v"(g));  // "0" leading test: entry 0 (see chunks)
-    const uint32_t c1 = last ? ((kLastPosEntry - (2u << kChunkBits)) | (g & 1u)) : (g & t & kChunkMask);
-    uint32_t a1;
-    asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a1) : "v"(c1), "s"(base));
-    return ((lds_u32*)(uintptr_t)a1)[2u << kChunkBits];
-  }
-  __device__ __forceinline__ uint32_t chunk1(uint32_t g, bool group) const {
-    const uint32_t base = (uint32_t)(uintptr_t)(lds_u32*)lut32;
-    uint32_t t;
-    asm("v_bfe_i32 %0, %1, 0, 1" : "=v"(t) : "v"(g));  // "0" leading test: entry 0 (see chunks)
-    const uint32_t c1 = group ? (g & t & kChunkMask) : kNoGroupEntry - (2u << kChunkBits);
-    uint32_t a1;
-    asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a1) : "v"(c1), "s"(base));
-    return ((lds_u32*)(uintptr_t)a1)[2u << kChunkBits];
+  __device__ __forceinline__ uint32_t chunk1_fast(uint32_t g) const {
+    return tab(2 * kStateBytes + off1(lead_masked(g)));
   }
   __device__ __forceinline__ void load() {
     const uint32_t* r = lds32 + (pos >> 5) * 64;
@@ -624,7 +607,8 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
   // to 16 to a bank).  Rows D .. D+4 are zero slack for the reader.  The
   // block's loads are issued first, then the workgroup's copy of the chunk
   // tables, so both latencies overlap before the one barrier.
-  uint32_t* lut = (uint32_t*)(lds_all + (size_t)(blockDim.x >> 6) * g.lds_words);
+  __shared__ __attribute__((aligned(16))) uint32_t ctab[kChunkLutBytes / 4];  // LDS address 0 (static)
+  uint32_t* lut = ctab;
   // (1D reads chunk-1 entries only: state 2 and the no-group entry)
   constexpr uint32_t kLutFrom = DIMS == 1 ? (2u << kChunkBits) / 4 : 0;
   const uint32_t* seg = (const uint32_t*)(stream + (size_t)wave * g.maxbits);
@@ -821,7 +805,7 @@ int launch_decode_t(const uint64_t* stream, const Geometry& g, bool fast, void* 
   if (reg) gg.lds_words = 0;
   const uint32_t wpg = waves_per_group(gg.lds_words, kChunkLutBytes);
   const dim3 grid((nwaves + wpg - 1) / wpg), block(kLanes * wpg);
-  const size_t lds = (size_t)wpg * gg.lds_words * 8 + kChunkLutBytes;
+  const size_t lds = (size_t)wpg * gg.lds_words * 8;  // (+ the static chunk tables)
   Scalar* d = (Scalar*)data;
   if constexpr (DIMS <= 2) {
     if (reg) {

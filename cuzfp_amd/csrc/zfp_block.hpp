@@ -42,6 +42,9 @@
 #ifndef ZFP_COUNT_PLANE  // host-side path statistics (tools/path_stats.cpp)
 #define ZFP_COUNT_PLANE(g0, fast, complete)
 #endif
+#ifndef ZFP_COUNT_PATH  // host-side decoder path statistics (tools/path_stats.cpp)
+#define ZFP_COUNT_PATH(id)
+#endif
 
 namespace cuzfp {
 
@@ -1051,9 +1054,6 @@ constexpr uint32_t kChunkMask = (1u << kChunkBits) - 1;
 constexpr unsigned kOnesShift = 15, kPosShift = 26;
 constexpr uint32_t kUsedMask = (1u << 14) - 1, kNotEnded = 1u << 13;
 constexpr uint32_t kEntryState = 1u << 31;
-// a last entry, for planes with no group part (n = N): ended, nothing used
-constexpr uint32_t kNoGroupEntry = 3u << kChunkBits;
-constexpr uint32_t kLastPosEntry = kNoGroupEntry + 2;  // and + 1
 
 constexpr uint32_t pack_entry(uint32_t ones, uint32_t pos, uint32_t used, uint32_t flags) {
   return (ones << kOnesShift) | (pos << kPosShift) | used | flags;
@@ -1091,23 +1091,28 @@ constexpr uint32_t chunk_entry(unsigned state, uint32_t b) {
 }
 
 struct ChunkLut {
-  uint32_t e[(3u << kChunkBits) + 4];  // [state][chunk], the no-group entry, padding to 16 B
+  uint32_t e[3u << kChunkBits];  // [state][chunk]
 };
 constexpr ChunkLut make_chunk_lut() {
   ChunkLut t{};
   for (unsigned s = 0; s < 3; s++)
     for (uint32_t b = 0; b <= kChunkMask; b++) t.e[(s << kChunkBits) | b] = chunk_entry(s, b);
-  t.e[kNoGroupEntry] = pack_entry(0, 0, 0, 0);
-  // n = N-1 (the fast decoder keeps n at most N-1): the group part is the
-  // last position's bit alone -- a "0" test, or a "1" test with the one at
-  // N-1 implied -- indexed by that bit (decode_plane_fast)
-  t.e[kLastPosEntry] = pack_entry(0, 0, 1, 0);
-  t.e[kLastPosEntry + 1] = pack_entry(1, 0, 1, 0);
   return t;
 }
 
 // m = 0 .. 64 low bits set
 ZFP_HD uint64_t lowmask64(unsigned m) { return m ? ~0ull >> ((64u - m) & 63u) : 0ull; }
+
+// (a & m) | c in one v_and_or_b32
+ZFP_HD uint32_t and_or(uint32_t a, uint32_t m, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t r;
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(m), "v"(c));
+  return r;
+#else
+  return (a & m) | c;
+#endif
+}
 
 // v when bit 13 of e is set, else 0 (v_bfe_i32 + v_and_b32)
 ZFP_HD uint32_t keep_if_bit13(uint32_t v, uint32_t e) {
@@ -1120,18 +1125,6 @@ ZFP_HD uint32_t keep_if_bit13(uint32_t v, uint32_t e) {
 #endif
 }
 
-// One plane by table lookup.  Reader: windows(m, w, g) gives the 64 stream
-// bits at the read position (w) and the 32 bits m further on (g);
-// chunks(g, group, e1, e2a, e2b) reads the entry of g's first chunk in state 2
-// (the no-group entry when !group) and of its second chunk in states 0 and 1;
-// chunk1(g, group) only the first.
-// Sets `slow` for a plane the tables cannot finish (a code longer than two
-// chunks, one that runs into the budget, or one that reaches position N-1,
-// where the one is implied); the caller then discards this step's result and
-// state and decodes the plane again with decode_plane.  So nothing here is
-// gated on `slow`: a lane out of budget (b1 = 0) reads zeros past its block
-// (its group test reads as a "0" it does not consume), and a plane with no
-// group part (n = N) looks up the empty entry.
 // v unless bit 13 of e is set (v_bfe_i32 + v_bfi_b32)
 ZFP_HD uint32_t drop_if_bit13(uint32_t v, uint32_t e) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -1165,13 +1158,22 @@ ZFP_HD uint32_t implied_end(uint32_t e1, uint32_t e2, uint32_t q, uint64_t& ones
   return o;
 }
 
+// One plane by table lookup, with the budget.  Reader: windows(m, w, g) gives
+// the 64 stream bits at the read position (w) and the 32 bits m further on
+// (g); chunks_fast(g, e1, e2a, e2b) reads the entry of g's first chunk in
+// state 2 and of its second chunk in states 0 and 1, chunk1_fast(g) only the
+// first; window32 / chunks_st read continuation pairs.  Sets `slow` for a
+// plane the tables cannot finish (see below); the caller then discards this
+// step's result and state and decodes the plane again with decode_plane.  So
+// nothing here is gated on `slow`: a lane out of budget (b1 = 0) reads zeros
+// past its block (its group test reads as a "0" it does not consume).
 template <int DIMS, typename PW, typename Reader>
 ZFP_HD PW decode_plane_lut(unsigned& bits, unsigned& n, Reader& rd, bool& slow) {
   constexpr unsigned N = 1u << (2 * DIMS);
-  // n is kept at most N-1: with n = N-1 the group part is the last
+  // n is taken as at most N-1: with n = N-1 the group part is the last
   // position's bit alone (a "0" test, or a "1" test with the one implied),
-  // which reads the same bits as N verbatim ones; two dedicated table entries
-  // decode it (kLastPosEntry)
+  // which reads the same bits as N verbatim ones; the implied-one rule below
+  // resolves it from the state-2 entry of that bit
   const unsigned nf = n < N - 1 ? n : N - 1;
   const unsigned m = umin(nf, bits);
   uint64_t w;
@@ -1184,92 +1186,28 @@ ZFP_HD PW decode_plane_lut(unsigned& bits, unsigned& n, Reader& rd, bool& slow) 
   uint32_t e1, e2;
   if constexpr (DIMS == 1) {
     // a 1D code (4 positions, at most 7 bits with the leading test) fits chunk 1
-    e1 = rd.chunk1_fast(g, nf == N - 1);
+    e1 = rd.chunk1_fast(g);
     e2 = 0;
   } else {
     uint32_t e2a, e2b;
-    rd.chunks_fast(g, nf == N - 1, e1, e2a, e2b);
-    const uint32_t e2s = (e1 & kEntryState) ? e2b : e2a;
-    e2 = keep_if_bit13(e2s, e1);  // nothing after a chunk 1 that ended
-  }
-  const uint32_t S = e1 + e2;                  // field-wise sums
-  const uint32_t npos = S >> kPosShift & 31u;
-  const uint32_t used = S & kUsedMask;         // >= kNotEnded: the code has not ended
-  const uint32_t ones = ((e1 >> kOnesShift) & kChunkMask) |
-                        (((e2 >> kOnesShift) & kChunkMask) << ((e1 >> kPosShift) & 31u));
-  // The stream reads as zeros past the block's last bit (the kernels and the
-  // host reader guarantee it) and the budget always ends there, so a code
-  // whose last one is the budget's last bit ends here one bit past the budget
-  // (its zero group test is not in the stream): the reference keeps that one
-  // and reads no more (decode.c:302-317).  Codes longer than the two chunks
-  // and codes the budget cuts short take decode_plane_cont; a code reaching
-  // position N-1 the general decoder.
-  slow = !(used <= b1 + 1 && npos <= N - 1 - nf);
-  uint64_t ones64 = ones;
-  uint32_t np = npos, take = umin(used, b1);
-  const uint32_t q = N - 1 - nf;
-  if (__builtin_expect(any_lane(npos > q), 0)) {  // the code reaches position N-1 (implied one)
-    if (npos > q) {
-      const uint32_t o = implied_end(e1, e2, q, ones64);
-      slow = o > b1;  // the budget runs out first: the general decoder
-      np = q + 1u;
-      take = o;
-    }
-  }
-  // the verbatim bits below m, the new ones at n >= m: one v_bfi_b32 a dword
-  // under the mask ~0 << m (m <= N-1)
-  const PW hi = (PW)(~0ull << m);
-  const PW x = (hi & ((PW)ones64 << nf)) | (~hi & (PW)w);
-  n = nf + np;
-  const unsigned adv = m + take;
-  rd.pos += adv;
-  bits -= adv;
-  return x;
-}
-
-// The table step for the planes decode_plane_lut leaves (a dense plane's
-// code longer than two chunks, or a code the budget cuts short): the same
-// first chunk pair, further pairs while the budget reaches past what has been
-// read, and the budget cut resolved from the table sums.  Sets `slow` for what
-// is left (a code reaching position N-1, where the one is implied) to the
-// general decoder.
-template <int DIMS, typename PW, typename Reader>
-ZFP_HD PW decode_plane_cont(unsigned& bits, unsigned& n, Reader& rd, bool& slow) {
-  constexpr unsigned N = 1u << (2 * DIMS);
-  const unsigned m = umin(n, bits);
-  uint64_t w;
-  uint32_t g;
-  rd.windows(m, w, g);
-  const uint64_t vmask = lowmask64(m);
-  const unsigned b1 = bits - m;                // budget after the verbatim bits
-  // chunk 1 starts at the leading group test (table state 2), chunk 2 is read
-  // in both states and chosen by chunk 1's exit state; nothing follows a
-  // chunk 1 that ended the code
-  uint32_t e1, e2;
-  if constexpr (DIMS == 1) {
-    // a 1D code (4 positions, at most 7 bits with the leading test) fits chunk 1
-    e1 = rd.chunk1(g, n < N);
-    e2 = 0;
-  } else {
-    uint32_t e2a, e2b;
-    rd.chunks(g, n < N, e1, e2a, e2b);
+    rd.chunks_fast(g, e1, e2a, e2b);
     const uint32_t e2s = (e1 & kEntryState) ? e2b : e2a;
     e2 = keep_if_bit13(e2s, e1);  // nothing after a chunk 1 that ended
   }
   const uint32_t S = e1 + e2;                  // field-wise sums
   uint32_t npos = S >> kPosShift & 31u;
-  const uint32_t used0 = S & kUsedMask;        // >= kNotEnded: the code has not ended
-  bool ended = used0 < kNotEnded;
-  uint32_t parsed = ended ? used0 : used0 - kNotEnded;  // code bits read (all of them if not ended)
+  const uint32_t used = S & kUsedMask;         // >= kNotEnded: the code has not ended
   uint64_t ones = ((e1 >> kOnesShift) & kChunkMask) |
                   (((e2 >> kOnesShift) & kChunkMask) << ((e1 >> kPosShift) & 31u));
-  uint32_t st = (DIMS == 1 ? e1 : e2) >> 31;  // exit state of the last chunk read (code not ended)
+  bool ended = used < kNotEnded;
+  uint32_t parsed = ended ? used : used - kNotEnded;  // code bits read (all of the chunks' if not ended)
+  uint32_t st = (DIMS == 1 ? e1 : e2) >> 31;          // exit state of the last chunk read
   if constexpr (DIMS >= 2) {
     // A code longer than the two chunks (a dense plane, the last few of a
     // block): further chunk pairs from the exit state, while the budget
     // reaches past what has been read.  In a continuation pair both chunks
     // are in state 0/1, whose entries carry the marker when they end.
-    bool open = !ended && parsed < b1 && n + npos < N;
+    bool open = !ended && parsed < b1 && nf + npos < N;
     if (__builtin_expect(any_lane(open), 0)) {
       while (any_lane(open)) {
         if (open) {
@@ -1286,7 +1224,7 @@ ZFP_HD PW decode_plane_cont(unsigned& bits, unsigned& n, Reader& rd, bool& slow)
           ended = u >= kNotEnded;
           parsed += u & (kNotEnded - 1u);
           st = eB >> 31;
-          open = !ended && parsed < b1 && n + npos < N;
+          open = !ended && parsed < b1 && nf + npos < N;
         }
       }
     }
@@ -1295,28 +1233,49 @@ ZFP_HD PW decode_plane_cont(unsigned& bits, unsigned& n, Reader& rd, bool& slow)
   // host reader guarantee it) and the budget always ends there.  So:
   //  - a code that ended within the budget, or one bit past it (a one read
   //    with the budget's last bit, followed by the zero group test that is
-  //    not in the stream), is taken as read;
-  //  - a code the budget cut short at a token boundary reads on as zero
+  //    not in the stream), is taken as read (decode.c:302-317);
+  //  - a code the budget cuts short inside the two chunks reads on as zero
   //    positions: the reference deposited one more one at the position it
-  //    had reached when the budget ran out (decode.c:305-311), and that
-  //    position is npos less the bits read past the budget.
-  // Positions must stay below N-1 (there the one is implied and not read);
-  // anything else takes the general decoder.  (N - 1 - n is huge for n = N.)
-  // (a code read up to the budget's last bit that ends there with a one --
-  // exit state 1, its group test past the block -- ended as read)
-  if (!ended && parsed == b1 && st) {
+  //    had reached when the budget ran out (decode.c:305-311), npos less the
+  //    bits read past the budget.
+  // A code whose parse reaches position N-1 (where the one is implied) is
+  // resolved from the first two chunks' entries if that happens within the
+  // budget; anything else left takes the general decoder.
+  if (!ended && parsed == b1 && st) {  // a one on the budget's last bit
     ended = true;
     parsed = b1 + 1u;
   }
+  const uint32_t q = N - 1 - nf;
   const bool cut = !ended && parsed >= b1;
-  const uint32_t P = cut ? npos - (parsed - b1) : npos;
-  slow = cut ? !(P <= N - 1 - n) : !(ended && parsed <= b1 + 1 && npos <= N - 1 - n);
-  ones |= (uint64_t)(cut ? 1u : 0u) << (P & 63u);
+  const uint32_t P = cut ? npos - (parsed - b1) : npos;  // cut: the position of the deposited one
+  slow = cut ? P > q : !(ended && parsed <= b1 + 1 && npos <= q);
+  uint64_t ones64 = ones | ((uint64_t)(cut ? 1u : 0u) << (P & 63u));
+  uint32_t np = cut ? P + 1u : npos, take = cut ? b1 : umin(parsed, b1);
+  if (__builtin_expect(any_lane(npos > q), 0)) {  // the parse reaches position N-1 (implied one)
+    if (npos > q) {
+      uint64_t o64 = ones;
+      const uint32_t o = implied_end(e1, e2, q, o64);
+      // position N-1 within the first two chunks and the budget: the code
+      // ends there; the budget running out first leaves the cut result above
+      // (slow unless its one lies at or below N-1); anything else takes the
+      // general decoder
+      if (o <= b1 && ((e1 >> kPosShift) & 31u) + ((e2 >> kPosShift) & 31u) > q) {
+        slow = false;
+        ones64 = o64;
+        np = q + 1u;
+        take = o;
+      } else if (!cut) {
+        slow = true;
+      }
+    }
+  }
+  ZFP_COUNT_PATH(slow ? (npos > q ? (cut ? 11 : 12) : (cut ? 13 : (!ended ? 14 : 15))) : 10);
   // the verbatim bits below m, the new ones at n >= m: one v_bfi_b32 a dword
-  const PW o = (PW)ones << (n & (8 * sizeof(PW) - 1));
-  const PW x = ((PW)vmask & (PW)w) | (~(PW)vmask & o);
-  n += cut ? P + 1u : npos;
-  const unsigned adv = m + (cut ? b1 : umin(parsed, b1));
+  // under the mask ~0 << m (m <= N-1)
+  const PW hi = (PW)(~0ull << m);
+  const PW x = (hi & ((PW)ones64 << nf)) | (~hi & (PW)w);
+  n = nf + np;
+  const unsigned adv = m + take;
   rd.pos += adv;
   bits -= adv;
   return x;
@@ -1331,30 +1290,35 @@ ZFP_HD PW decode_plane_cont(unsigned& bits, unsigned& n, Reader& rd, bool& slow)
 // code longer than two chunks or one reaching position N-1; the caller then
 // decodes that plane again with the budget-aware steps.
 template <int DIMS, typename PW, typename Reader>
-ZFP_HD PW decode_plane_fast(unsigned& bits, unsigned& n, Reader& rd, bool& slow) {
+ZFP_HD PW decode_plane_fast(unsigned& bits, unsigned& n, Reader& rd, bool& slow, bool& rare) {
   constexpr unsigned N = 1u << (2 * DIMS);
   const unsigned nf = n < N - 1 ? n : N - 1;
   uint64_t w;
   uint32_t g;
   rd.windows(nf, w, g);
   uint32_t e1, e2a, e2b;
-  rd.chunks_fast(g, nf == N - 1, e1, e2a, e2b);
+  rd.chunks_fast(g, e1, e2a, e2b);
   const uint32_t e2 = keep_if_bit13((e1 & kEntryState) ? e2b : e2a, e1);
   const uint32_t S = e1 + e2;
   const uint32_t npos = S >> kPosShift & 31u;
   const uint32_t used = S & kUsedMask;
   const uint32_t ones = ((e1 >> kOnesShift) & kChunkMask) |
                         (((e2 >> kOnesShift) & kChunkMask) << ((e1 >> kPosShift) & 31u));
-  slow = used >= kNotEnded || npos > N - 1 - nf;
   uint64_t ones64 = ones;
   uint32_t np = npos, take = used;
   const uint32_t q = N - 1 - nf;
-  if (__builtin_expect(any_lane(npos > q), 0)) {  // the code reaches position N-1 (implied one)
-    if (npos > q) {
+  // One wave-uniform test for both rare cases: a code longer than the two
+  // chunks (the sum carries the marker) and one reaching position N-1
+  // (nf + npos >= N; nf + npos < 2N).
+  slow = false;
+  rare = any_lane(and_or(S, kNotEnded, nf + npos) >= N);  // (nf + npos < 2N)
+  if (__builtin_expect(rare, 0)) {
+    const bool implied = npos > q;
+    if (implied) {  // the code reaches position N-1: the one there is implied
       take = implied_end(e1, e2, q, ones64);  // within the budget (fast_room)
       np = q + 1u;
-      slow = false;
     }
+    slow = !implied && used >= kNotEnded;  // longer than two chunks: decode_plane_lut
   }
   // bits >= nf of the plane from the group code, below it verbatim: one
   // v_bfi_b32 a dword under the mask ~0 << nf
@@ -1389,20 +1353,13 @@ ZFP_HD PW decode_plane_any(unsigned& bits, unsigned& n, Reader& rd) {
   const unsigned n0 = n, bits0 = bits;
   bool slow;
   PW x = decode_plane_lut<DIMS, PW>(bits, n, rd, slow);
-  if (__builtin_expect(any_lane(slow), 0)) {  // wave-uniform test first (see encode_plane_any)
+  ZFP_COUNT_PATH(slow ? 6 : 5);
+  if (__builtin_expect(any_lane(slow), 0)) {  // wave-uniform test first: the per-lane branch costs exec-mask work
     if (slow) {
       rd.init(pos0);
       n = n0;
       bits = bits0;
-      x = decode_plane_cont<DIMS, PW>(bits, n, rd, slow);
-    }
-    if (__builtin_expect(any_lane(slow), 0)) {
-      if (slow) {
-        rd.init(pos0);
-        n = n0;
-        bits = bits0;
-        x = decode_plane<DIMS, PW>(bits, n, rd);
-      }
+      x = decode_plane<DIMS, PW>(bits, n, rd);
     }
   }
   return x;
@@ -1414,14 +1371,16 @@ template <int DIMS, typename PW, typename Reader>
 ZFP_HD PW decode_plane_fast_any(unsigned& bits, unsigned& n, Reader& rd) {
   const auto pos0 = rd.pos;
   const unsigned n0 = n, bits0 = bits;
-  bool slow;
-  PW x = decode_plane_fast<DIMS, PW>(bits, n, rd, slow);
-  if (__builtin_expect(any_lane(slow), 0)) {
+  bool slow, rare;
+  PW x = decode_plane_fast<DIMS, PW>(bits, n, rd, slow, rare);
+  ZFP_COUNT_PATH(slow ? 2 : rare ? 1 : 0);
+  if (__builtin_expect(rare, 0) && any_lane(slow)) {
     if (slow) {
       rd.init(pos0);
       n = n0;
       bits = bits0;
-      x = decode_plane_cont<DIMS, PW>(bits, n, rd, slow);
+      x = decode_plane_lut<DIMS, PW>(bits, n, rd, slow);
+      ZFP_COUNT_PATH(slow ? 3 : 4);
     }
     if (__builtin_expect(any_lane(slow), 0)) {
       if (slow) {
