@@ -262,7 +262,18 @@ ZFP_HD void inv_xform(UInt* p) {
 // column R*s + j of the input, i.e. plane (R*s + j) of R coefficients.  The
 // operation is an involution, so the decoder uses it unchanged.
 
-// (a & m) | (b & ~m)
+// (a & m) | (b & ~m), m in a VGPR
+ZFP_HD uint32_t bfi_v(uint32_t m, uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+  return r;
+#else
+  return (a & m) | (b & ~m);
+#endif
+}
+
+// (a & m) | (b & ~m), m a wave-uniform constant (SGPR)
 ZFP_HD uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {
 #if defined(__HIP_DEVICE_COMPILE__)
   uint32_t r;
@@ -679,14 +690,28 @@ ZFP_HD uint32_t low_bits(uint32_t v, uint32_t w) {
 // alone either way (a "1" test with the one implied, or a "0" test), so the
 // plane codes are those of n = N, verbatim.  Requires width <= 31, which
 // holds for r < 2^15 (3D: checked by the caller) and always in 1D/2D.
+struct PlaneLen {  // the one-put step's lengths (plane_len)
+  uint32_t nn, imp, width, len;
+};
+// nn = n + bitlen(r) <= N, imp = r's top one at N-1 (it is implied), width =
+// the group code's bits after the leading "1" (L = bitlen + popcount, less the
+// implied one), len = the whole plane code: n verbatim bits, "1", width bits,
+// the closing "0" unless imp.  Computed once and shared by the fit test, the
+// put and the next plane's n (the compiler does not merge 2*imp with imp).
+template <int DIMS>
+ZFP_HD PlaneLen plane_len(uint32_t nf, uint32_t bl, uint32_t L) {
+  PlaneLen p;
+  p.nn = nf + bl;
+  p.imp = p.nn >> (2 * DIMS);
+  p.width = L - p.imp;
+  p.len = nf + p.width + 1u - p.imp;
+  return p;
+}
+
 template <int DIMS, typename PW, typename Writer>
-ZFP_HD void encode_plane_one_put(PW x, unsigned nf, uint32_t rl, uint32_t bl, uint32_t L, unsigned& n,
-                                 Writer& wr) {
+ZFP_HD void encode_plane_one_put(PW x, unsigned nf, uint32_t rl, const PlaneLen& pl, unsigned& n, Writer& wr) {
   constexpr unsigned N = 1u << (2 * DIMS);
-  const uint32_t nn = nf + bl;           // <= N
-  const uint32_t imp = nn >> (2 * DIMS);  // r's top one at N-1
-  const uint32_t width = L - imp;
-  const uint32_t len = nf + width + 1u - imp;
+  const uint32_t width = pl.width;
   // "1" + r with every one doubled: one table entry a byte of r (3D: r < 2^15,
   // 2D: r < 2^16; where r's top bits move past bit 31 they lie past width)
   const uint32_t e0 = wr.sp0(byte_off4<0>(rl));
@@ -694,8 +719,8 @@ ZFP_HD void encode_plane_one_put(PW x, unsigned nf, uint32_t rl, uint32_t bl, ui
   if constexpr (N > 4) G |= wr.sp1(byte_off4<1>(rl)) << (e0 & 31u);
   const uint32_t g = low_bits(G, width);
   const uint64_t code = (uint64_t)x ^ ((uint64_t)(rl ^ g) << nf);
-  wr.put(code, len);
-  n = nn - imp;  // min(nn, N-1)
+  wr.put(code, pl.len);
+  n = pl.nn - pl.imp;  // min(nn, N-1)
 }
 
 // r with every one doubled, for a 32-bit r: four byte lookups placed at
@@ -759,17 +784,17 @@ ZFP_HD void encode_plane_step(PW x, unsigned& n, Writer& wr) {
   const uint32_t rl = (uint32_t)r;
   const uint32_t bl = bitlen16(rl);
   const uint32_t L = (uint32_t)__builtin_popcount(rl) + bl;  // v_bcnt_u32_b32(rl, bl)
+  const PlaneLen pl = plane_len<DIMS>(nf, bl, L);
   if constexpr (N <= 16) {
     // r has at most 16 bits and the code at most 48: always one put
-    encode_plane_one_put<DIMS>(x, nf, rl, bl, L, n, wr);
+    encode_plane_one_put<DIMS>(x, nf, rl, pl, n, wr);
   } else {
     // one put while every lane's code fits 64 bits with r < 2^15 (3D rate 8
     // on smooth data: ~26 of ~29 plane steps, tools/coder_stats.cpp);
     // otherwise the wide step for the whole wave
-    const uint32_t imp = (nf + bl) >> 6;
-    const bool ok = (r >> 15) == 0 && nf + L + 1u - 2u * imp <= 64u;
+    const bool ok = (r >> 15) == 0 && pl.len <= 64u;
     if (__builtin_expect(!any_lane(!ok), 1))
-      encode_plane_one_put<DIMS>(x, nf, rl, bl, L, n, wr);
+      encode_plane_one_put<DIMS>(x, nf, rl, pl, n, wr);
     else
       encode_plane_wide((uint64_t)x, n, wr);
   }
@@ -1103,6 +1128,19 @@ constexpr ChunkLut make_chunk_lut() {
 // m = 0 .. 64 low bits set
 ZFP_HD uint64_t lowmask64(unsigned m) { return m ? ~0ull >> ((64u - m) & 63u) : 0ull; }
 
+// (ones << s) above bit s, w below it: the mask ~0 << s, the shift, and one
+// v_bfi_b32 a dword (the compiler's form of the same expression ORs the
+// shifted ones in after the insert: two more instructions)
+template <typename PW>
+ZFP_HD PW merge_at(uint32_t s, uint64_t ones, uint64_t w) {
+  const uint64_t hi = ~0ull << s, o = ones << s;
+  if constexpr (sizeof(PW) == 8)
+    return (PW)bfi_v((uint32_t)hi, (uint32_t)o, (uint32_t)w) |
+           ((PW)bfi_v((uint32_t)(hi >> 32), (uint32_t)(o >> 32), (uint32_t)(w >> 32)) << 32);
+  else
+    return (PW)bfi_v((uint32_t)hi, (uint32_t)o, (uint32_t)w);
+}
+
 // (a & m) | c in one v_and_or_b32
 ZFP_HD uint32_t and_or(uint32_t a, uint32_t m, uint32_t c) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -1322,8 +1360,7 @@ ZFP_HD PW decode_plane_fast(unsigned& bits, unsigned& n, Reader& rd, bool& slow,
   }
   // bits >= nf of the plane from the group code, below it verbatim: one
   // v_bfi_b32 a dword under the mask ~0 << nf
-  const PW hi = (PW)(~0ull << nf);
-  const PW x = (hi & ((PW)ones64 << nf)) | (~hi & (PW)w);
+  const PW x = merge_at<PW>(nf, ones64, w);
   n = nf + np;
   const unsigned adv = nf + take;
 #if defined(CUZFP_EXP_DEC_EXTRA_RT)  // timing experiment: one more dependent LDS round trip a plane
