@@ -1240,6 +1240,10 @@ ZFP_HD PW decode_plane_lut(unsigned& bits, unsigned& n, Reader& rd, bool& slow) 
   bool ended = used < kNotEnded;
   uint32_t parsed = ended ? used : used - kNotEnded;  // code bits read (all of the chunks' if not ended)
   uint32_t st = (DIMS == 1 ? e1 : e2) >> 31;          // exit state of the last chunk read
+  const uint32_t q = N - 1 - nf;
+  // the code bits up to position N-1's token when a continuation pair reaches
+  // it (the first pair's case is implied_end below)
+  uint32_t io = 0;
   if constexpr (DIMS >= 2) {
     // A code longer than the two chunks (a dense plane, the last few of a
     // block): further chunk pairs from the exit state, while the budget
@@ -1255,7 +1259,16 @@ ZFP_HD PW decode_plane_lut(unsigned& bits, unsigned& n, Reader& rd, bool& slow) 
           const uint32_t eB = drop_if_bit13((eA & kEntryState) ? eBb : eBa, eA);
           const uint32_t T = eA + eB;
           const uint32_t pA = (eA >> kPosShift) & 31u;
-          const uint64_t o = ((eA >> kOnesShift) & kChunkMask) | (((eB >> kOnesShift) & kChunkMask) << pA);
+          const uint32_t oA = (eA >> kOnesShift) & kChunkMask, oB = (eB >> kOnesShift) & kChunkMask;
+          const uint64_t o = oA | ((uint64_t)oB << pA);
+          // this pair reaches position N-1 (offset q2 into it): the code ends
+          // at the start of that position's token -- st + q2 + the ones'
+          // "more" bits below it in chunk A, or chunk A whole and the same
+          // count in chunk B (as implied_end for the first pair)
+          const uint32_t q2 = q - npos;  // npos <= q while open
+          io = pA > q2 ? parsed + st + q2 + (uint32_t)__builtin_popcount(oA & ((1u << q2) - 1u))
+                       : parsed + kChunkBits + (eA >> 31) + (q2 - pA) +
+                             (uint32_t)__builtin_popcount(oB & ((1u << ((q2 - pA) & 31u)) - 1u));
           ones |= o << (npos & 63u);
           npos += (T >> kPosShift) & 31u;
           const uint32_t u = T & kUsedMask;
@@ -1283,7 +1296,6 @@ ZFP_HD PW decode_plane_lut(unsigned& bits, unsigned& n, Reader& rd, bool& slow) 
     ended = true;
     parsed = b1 + 1u;
   }
-  const uint32_t q = N - 1 - nf;
   const bool cut = !ended && parsed >= b1;
   const uint32_t P = cut ? npos - (parsed - b1) : npos;  // cut: the position of the deposited one
   slow = cut ? P > q : !(ended && parsed <= b1 + 1 && npos <= q);
@@ -1292,12 +1304,13 @@ ZFP_HD PW decode_plane_lut(unsigned& bits, unsigned& n, Reader& rd, bool& slow) 
   if (__builtin_expect(any_lane(npos > q), 0)) {  // the parse reaches position N-1 (implied one)
     if (npos > q) {
       uint64_t o64 = ones;
-      const uint32_t o = implied_end(e1, e2, q, o64);
-      // position N-1 within the first two chunks and the budget: the code
-      // ends there; the budget running out first leaves the cut result above
-      // (slow unless its one lies at or below N-1); anything else takes the
-      // general decoder
-      if (o <= b1 && ((e1 >> kPosShift) & 31u) + ((e2 >> kPosShift) & 31u) > q) {
+      uint32_t o = implied_end(e1, e2, q, o64);
+      // reached in a continuation pair: its count from the loop
+      if (((e1 >> kPosShift) & 31u) + ((e2 >> kPosShift) & 31u) <= q) o = io;
+      // position N-1 within the budget: the code ends there; the budget
+      // running out first leaves the cut result above (slow unless its one
+      // lies at or below N-1)
+      if (o <= b1) {
         slow = false;
         ones64 = o64;
         np = q + 1u;

@@ -24,6 +24,13 @@ for s in $STEPS; do
       # the parity subset that exercises every coder path (golden BASELINE streams, fuzz, extremes, random streams)
       timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -m gpu -x -q -p no:cacheprovider -k "golden_baseline or fuzz_vs_oracle or extreme or random_streams or golden_fuzz" > "$OUT/pytest_quick_$TAG.log" 2>&1
       ok_or_stop $? quick; tail -3 "$OUT/pytest_quick_$TAG.log" ;;
+    g1024)
+      # BASELINE configs[4] parity: the whole 1024^3 array and its slabs against the reference's hashes
+      timeout -k 10 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider -k "1024" > "$OUT/pytest_1024_$TAG.log" 2>&1
+      ok_or_stop $? g1024; tail -3 "$OUT/pytest_1024_$TAG.log" ;;
+    stepgap)
+      timeout -k 10 300 python tools/step_gap.py > "$OUT/stepgap_$TAG.txt" 2>&1
+      ok_or_stop $? stepgap; cat "$OUT/stepgap_$TAG.txt" ;;
     benchq)
       timeout -k 10 300 python bench.py --no-cpu-baseline --no-host-path > "$OUT/benchq_$TAG.json" 2> "$OUT/benchq_$TAG.err"
       ok_or_stop $? benchq; python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('value', d['value'], 'enc', d['encode_ms'], 'dec', d['decode_ms'], d['parity'])" "$OUT/benchq_$TAG.json" ;;
