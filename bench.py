@@ -52,8 +52,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=50)
     p.add_argument("--size", type=int, default=256, help="per-GPU array edge (cube edge in 3D)")
     p.add_argument("--dims", type=int, default=3, choices=[1, 2, 3],
                    help="1D / 2D arrays of edge --size (BASELINE configs 2D 8192^2 r2, 1D 1M r8); "
@@ -338,9 +338,13 @@ def main():
 
     per_graph = next(c for c in (10, 5, 4, 2, 1) if args.steps % c == 0)
     run = graphed(step, per_graph)
-    for _ in range(args.warmup):
+    # W warmup steps, replayed as the timed steps are (the last W % per_graph eagerly)
+    for _ in range(args.warmup // per_graph):
+        run()
+    for _ in range(args.warmup % per_graph):
         step()
-    run()
+    if args.warmup < per_graph:
+        run()  # the graph's first replay uploads it: never inside the timed region
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -351,6 +351,23 @@ constexpr bool kNtValues = true;
 #else
 constexpr bool kNtValues = false;  // A/B builds
 #endif
+// A/B builds: the gathers (CUZFP_TEMPORAL_LOADS) or the value stores
+// (CUZFP_TEMPORAL_STORES) alone without the hint
+#ifndef CUZFP_TEMPORAL_LOADS
+constexpr bool kNtLoads = kNtValues;
+#else
+constexpr bool kNtLoads = false;
+#endif
+#ifndef CUZFP_TEMPORAL_STORES
+constexpr bool kNtStores = kNtValues;
+#else
+constexpr bool kNtStores = false;
+#endif
+#ifndef CUZFP_NT_STREAM
+constexpr bool kNtStream = false;
+#else
+constexpr bool kNtStream = true;  // A/B builds: the compressed stream with the hint
+#endif
 template <bool NT>
 __device__ __forceinline__ uint4 ld16(const void* p) {
   if constexpr (NT) {
@@ -371,7 +388,7 @@ __device__ __forceinline__ void st16(void* p, uint4 v) {
 template <typename Scalar>
 __device__ __forceinline__ void load_row(const Scalar* p, Scalar* f) {
   if constexpr (sizeof(Scalar) == 4) {
-    const uint4 v = ld16<kNtValues>(p);
+    const uint4 v = ld16<kNtLoads>(p);
     __builtin_memcpy(f, &v, 16);
   } else {
     const uint4 a = ld16<false>(p);
@@ -386,7 +403,7 @@ __device__ __forceinline__ void store_row(Scalar* p, const Scalar* f) {
   if constexpr (sizeof(Scalar) == 4) {
     uint4 v;
     __builtin_memcpy(&v, f, 16);
-    st16<kNtValues>(p, v);
+    st16<kNtStores>(p, v);
   } else {
     uint4 a, b;
     __builtin_memcpy(&a, f, 16);
@@ -570,7 +587,7 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS, t
           const uint64_t a0 = mine[j * 64], a1 = mine[(j + 1) * 64];
           __builtin_memcpy(&v.x, &a0, 8);
           __builtin_memcpy(&v.z, &a1, 8);
-          *(uint4*)&dst[j] = v;
+          st16<kNtStream>(&dst[j], v);
         }
       } else {
         for (uint32_t j = 0; j < W; j++) dst[j] = mine[j * 64];
@@ -638,7 +655,7 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
       const uint4* src = (const uint4*)(seg + lane * D);
 #pragma unroll
       for (uint32_t q = 0; q < kHeld; q++)
-        if (4 * q < D) held[q] = src[q];
+        if (4 * q < D) held[q] = ld16<kNtStream>(&src[q]);
     }
     for (uint32_t i = kLutFrom + threadIdx.x; i < sizeof(ChunkLut) / 16; i += blockDim.x)
       ((uint4*)lut)[i] = ((const uint4*)g_chunk_lut.e)[i];

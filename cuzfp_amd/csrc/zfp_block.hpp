@@ -1238,7 +1238,7 @@ ZFP_HD PW decode_plane_lut(unsigned& bits, unsigned& n, Reader& rd, bool& slow) 
   uint64_t ones = ((e1 >> kOnesShift) & kChunkMask) |
                   (((e2 >> kOnesShift) & kChunkMask) << ((e1 >> kPosShift) & 31u));
   bool ended = used < kNotEnded;
-  uint32_t parsed = ended ? used : used - kNotEnded;  // code bits read (all of the chunks' if not ended)
+  uint32_t parsed = used & (kNotEnded - 1u);  // code bits read (all of the chunks' if not ended)
   uint32_t st = (DIMS == 1 ? e1 : e2) >> 31;          // exit state of the last chunk read
   const uint32_t q = N - 1 - nf;
   // the code bits up to position N-1's token when a continuation pair reaches
@@ -1292,15 +1292,16 @@ ZFP_HD PW decode_plane_lut(unsigned& bits, unsigned& n, Reader& rd, bool& slow) 
   // A code whose parse reaches position N-1 (where the one is implied) is
   // resolved from the first two chunks' entries if that happens within the
   // budget; anything else left takes the general decoder.
-  if (!ended && parsed == b1 && st) {  // a one on the budget's last bit
-    ended = true;
-    parsed = b1 + 1u;
-  }
-  const bool cut = !ended && parsed >= b1;
-  const uint32_t P = cut ? npos - (parsed - b1) : npos;  // cut: the position of the deposited one
-  slow = cut ? P > q : !(ended && parsed <= b1 + 1 && npos <= q);
+  // (bitwise rather than short-circuit logic below: one mask each, no
+  // divergent branches)
+  const uint32_t d = parsed - b1;  // code bits parsed past the budget (wraps when within)
+  // a one on the budget's last bit (its group test unread) also ends the code
+  const bool done = ended | ((d == 0u) & (st != 0u));
+  const bool cut = !done & ((int32_t)d >= 0);
+  const uint32_t P = npos - (cut ? d : 0u);  // cut: the position of the deposited one
+  slow = (cut & (P > q)) | (!cut & (!done | ((int32_t)d > 1) | (npos > q)));
   uint64_t ones64 = ones | ((uint64_t)(cut ? 1u : 0u) << (P & 63u));
-  uint32_t np = cut ? P + 1u : npos, take = cut ? b1 : umin(parsed, b1);
+  uint32_t np = P + (cut ? 1u : 0u), take = umin(parsed, b1);
   if (__builtin_expect(any_lane(npos > q), 0)) {  // the parse reaches position N-1 (implied one)
     if (npos > q) {
       uint64_t o64 = ones;

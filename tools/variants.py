@@ -51,12 +51,15 @@ x = torch.from_numpy(arr).cuda()
 mb = cz.rate_to_maxbits({rate}, arr.dtype, 3)
 w = cz.encode(x, mb); y = cz.decode(w, shape, x.dtype, mb)
 def t(fn):
-    for _ in range(5): fn()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(20): fn()
+    g.replay(); torch.cuda.synchronize()
     e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
     r = []
-    for _ in range(11):  # median of 11 batches of 40
+    for _ in range(11):  # median of 11 batches of 2 x 20 (hipGraph replays)
         torch.cuda.synchronize(); e0.record()
-        for _ in range(40): fn()
+        g.replay(); g.replay()
         e1.record(); torch.cuda.synchronize()
         r.append(e0.elapsed_time(e1) / 40 * 1000)
     return round(sorted(r)[5], 2)
