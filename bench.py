@@ -69,6 +69,8 @@ def parse():
     p.add_argument("--no-host-path", action="store_true")
     p.add_argument("--no-copy-probe", action="store_true", help="skip the device-to-device copy bandwidth probe")
     p.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
+    p.add_argument("--per-graph", type=int, default=0,
+                   help="steps captured per hipGraph (default: the largest divisor of --steps up to 200)")
     p.add_argument("--no-config5", action="store_true", help="skip BASELINE configs[4] (1024^3 sharded)")
     p.add_argument("--config5-edge", type=int, default=1024, help="edge of configs[4]'s global array")
     p.add_argument("--config5-steps", type=int, default=10)
@@ -336,7 +338,9 @@ def main():
             got = hashlib.sha256(words.cpu().numpy().tobytes()).hexdigest()
             parity = "stream sha256 == reference zfp 0.5.0" if got == rec["stream_sha256"] else "MISMATCH"
 
-    per_graph = next(c for c in (10, 5, 4, 2, 1) if args.steps % c == 0)
+    per_graph = args.per_graph or next(c for c in range(min(200, args.steps), 0, -1) if args.steps % c == 0)
+    if args.steps % per_graph:
+        raise SystemExit(f"--per-graph {per_graph} does not divide --steps {args.steps}")
     run = graphed(step, per_graph)
     # W warmup steps, replayed as the timed steps are (the last W % per_graph eagerly)
     for _ in range(args.warmup // per_graph):
@@ -367,20 +371,20 @@ def main():
     gpu_ms_per_step = ev0.elapsed_time(ev1) / args.steps
 
     # per-kernel durations with HIP events on the launch stream
-    def time_kernel(fn, reps):
-        r = graphed(fn, 10)
+    def time_kernel(fn, reps):  # reps launches as hipGraphs of 50
+        r = graphed(fn, 50)
         r()
         torch.cuda.synchronize()
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record(stream)
-        for _ in range(reps // 10):
+        for _ in range(reps // 50):
             r()
         e1.record(stream)
         torch.cuda.synchronize()
-        return e0.elapsed_time(e1) / (reps // 10 * 10)
+        return e0.elapsed_time(e1) / (reps // 50 * 50)
 
-    reps = 10 * max(2, args.steps // 10)
+    reps = 50 * max(2, args.steps // 50)
     enc_ms = time_kernel(lambda: cz.encode(x, maxbits, out=words), reps)
     dec_ms = time_kernel(lambda: cz.decode(words, shape, x.dtype, maxbits, out=y), reps)
 
