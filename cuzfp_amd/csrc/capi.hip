@@ -35,6 +35,9 @@ static int make_problem(int type, unsigned nx, unsigned ny, unsigned nz, long lo
   const uint64_t nb = (uint64_t)g.bx * g.by * ((g.nz + 3) / 4);
   if (nb >= (1ull << 32) - kLanes) return CUZFP_ERROR_INVALID_ARGUMENT;
   g.nblocks = (uint32_t)nb;
+  set_divisor(g.bx, g.dbx_m, g.dbx_s);
+  set_divisor(g.bx * g.by, g.dpl_m, g.dpl_s);
+  g.divmagic = nb < (1ull << 31) ? 1u : 0u;
   g.maxbits = maxbits;
   g.wave0 = 0;
   g.vec_io = 0;

@@ -417,18 +417,25 @@ struct BlockPos {
   uint32_t ix, iy, iz;
 };
 
+__device__ __forceinline__ uint32_t div_magic(uint32_t n, uint32_t m, uint32_t s) {
+  return (uint32_t)(((uint64_t)n * m) >> s);
+}
+
+// (the divisions by multiply-high with the launch's magic numbers: about a
+// dozen VALU instructions fewer each than the compiler's division)
 template <int DIMS>
 __device__ __forceinline__ BlockPos block_pos(const Geometry& g, uint32_t b) {
   BlockPos p;
   if constexpr (DIMS == 1) {
     p.ix = b; p.iy = 0; p.iz = 0;
   } else if constexpr (DIMS == 2) {
-    p.iy = b / g.bx; p.ix = b - p.iy * g.bx; p.iz = 0;
+    p.iy = g.divmagic ? div_magic(b, g.dbx_m, g.dbx_s) : b / g.bx;
+    p.ix = b - p.iy * g.bx; p.iz = 0;
   } else {
     const uint32_t plane = g.bx * g.by;
-    p.iz = b / plane;
+    p.iz = g.divmagic ? div_magic(b, g.dpl_m, g.dpl_s) : b / plane;
     const uint32_t r = b - p.iz * plane;
-    p.iy = r / g.bx;
+    p.iy = g.divmagic ? div_magic(r, g.dbx_m, g.dbx_s) : r / g.bx;
     p.ix = r - p.iy * g.bx;
   }
   return p;

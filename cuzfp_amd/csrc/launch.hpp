@@ -20,7 +20,22 @@ struct Geometry {
   uint32_t vec_io;       // stream base 16-byte aligned and maxbits even
   uint32_t lds_words;    // LDS words per wave
   int64_t sx, sy, sz;    // element strides
+  // block index -> position without an integer divide: q = (n * m) >> s for
+  // n < 2^31 (set_divisor), by bx and by bx * by; divmagic = 0 when nblocks
+  // is too large for it (plain division then)
+  uint32_t dbx_m, dbx_s, dpl_m, dpl_s, divmagic;
 };
+
+// q = floor(n / d) = (n * m) >> s for every n < 2^31, with s = 31 + ceil(log2 d)
+// and m = ceil(2^s / d) < 2^32: m = (2^s + e) / d with 0 <= e < d, so
+// n * m / 2^s = n / d + n e / (d 2^s) and n e < 2^31 * 2^ceil(log2 d) = 2^s
+// keeps the error below 1 / d, inside the gap floor(n / d) leaves.
+inline void set_divisor(uint32_t d, uint32_t& m, uint32_t& s) {
+  uint32_t l = 0;
+  while ((1ull << l) < d) l++;
+  s = 31 + l;
+  m = (uint32_t)(((1ull << s) + d - 1) / d);
+}
 
 struct Problem {
   int type;

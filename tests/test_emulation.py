@@ -172,3 +172,13 @@ def test_table_plane_decoder_fuzz(emu, dims):
     emu.emu_fuzz_plane.restype = ctypes.c_longlong
     emu.emu_fuzz_plane.argtypes = [ctypes.c_ulonglong, ctypes.c_longlong, ctypes.c_int]
     assert emu.emu_fuzz_plane(1234 + dims, 2_000_000, dims) == 0
+
+
+def test_block_index_division_magic(tmp_path):
+    """The launch's multiply-shift division of block indices (launch.hpp
+    set_divisor, used by block_pos for n < 2^31) equals integer division."""
+    exe = str(tmp_path / "divmagic")
+    subprocess.check_call(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "-o", exe,
+                           os.path.join(ROOT, "tests", "native", "divmagic.cpp")])
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and out.stdout.strip() == "0", out.stdout + out.stderr
