@@ -1205,33 +1205,17 @@ ZFP_HD uint32_t implied_end(uint32_t e1, uint32_t e2, uint32_t q, uint64_t& ones
 // step's result and state and decodes the plane again with decode_plane.  So
 // nothing here is gated on `slow`: a lane out of budget (b1 = 0) reads zeros
 // past its block (its group test reads as a "0" it does not consume).
+// The budget-aware step's resolution from the first pair's entries (e1, e2 as
+// chunks_fast and the exit-state select give them) and the verbatim window w
+// at the read position; nf = min(n, N-1), m = min(nf, bits).  Shared by
+// decode_plane_lut and the fast step's rare branch , which
+// reads the group window at nf rather than m: when m < nf both lie past the
+// block's end and read zeros.
 template <int DIMS, typename PW, typename Reader>
-ZFP_HD PW decode_plane_lut(unsigned& bits, unsigned& n, Reader& rd, bool& slow) {
+ZFP_HD PW lut_finish(unsigned& bits, unsigned& n, Reader& rd, bool& slow, unsigned nf, unsigned m,
+                     uint64_t w, uint32_t e1, uint32_t e2) {
   constexpr unsigned N = 1u << (2 * DIMS);
-  // n is taken as at most N-1: with n = N-1 the group part is the last
-  // position's bit alone (a "0" test, or a "1" test with the one implied),
-  // which reads the same bits as N verbatim ones; the implied-one rule below
-  // resolves it from the state-2 entry of that bit
-  const unsigned nf = n < N - 1 ? n : N - 1;
-  const unsigned m = umin(nf, bits);
-  uint64_t w;
-  uint32_t g;
-  rd.windows(m, w, g);
   const unsigned b1 = bits - m;                // budget after the verbatim bits
-  // chunk 1 starts at the leading group test (table state 2), chunk 2 is read
-  // in both states and chosen by chunk 1's exit state; nothing follows a
-  // chunk 1 that ended the code
-  uint32_t e1, e2;
-  if constexpr (DIMS == 1) {
-    // a 1D code (4 positions, at most 7 bits with the leading test) fits chunk 1
-    e1 = rd.chunk1_fast(g);
-    e2 = 0;
-  } else {
-    uint32_t e2a, e2b;
-    rd.chunks_fast(g, e1, e2a, e2b);
-    const uint32_t e2s = (e1 & kEntryState) ? e2b : e2a;
-    e2 = keep_if_bit13(e2s, e1);  // nothing after a chunk 1 that ended
-  }
   const uint32_t S = e1 + e2;                  // field-wise sums
   uint32_t npos = S >> kPosShift & 31u;
   const uint32_t used = S & kUsedMask;         // >= kNotEnded: the code has not ended
@@ -1333,14 +1317,39 @@ ZFP_HD PW decode_plane_lut(unsigned& bits, unsigned& n, Reader& rd, bool& slow) 
   return x;
 }
 
-// Table step without the budget (the decoder's common case, 3D): when every
-// lane of the wave has budget for the plane's longest table-decodable code
-// (N-1 verbatim bits + a two-chunk group code), the reads need no clipping
-// and no lane's budget can end inside the plane.  n is kept at most N-1 (with
-// n = N-1 the group part is the last position's bit alone, looked up in two
-// dedicated entries), so the verbatim mask is one shift.  Sets `slow` for a
-// code longer than two chunks or one reaching position N-1; the caller then
-// decodes that plane again with the budget-aware steps.
+template <int DIMS, typename PW, typename Reader>
+ZFP_HD PW decode_plane_lut(unsigned& bits, unsigned& n, Reader& rd, bool& slow) {
+  constexpr unsigned N = 1u << (2 * DIMS);
+  // n is taken as at most N-1: with n = N-1 the group part is the last
+  // position's bit alone (a "0" test, or a "1" test with the one implied),
+  // which reads the same bits as N verbatim ones; the implied-one rule
+  // resolves it from the state-2 entry of that bit
+  const unsigned nf = n < N - 1 ? n : N - 1;
+  const unsigned m = umin(nf, bits);
+  uint64_t w;
+  uint32_t g;
+  rd.windows(m, w, g);
+  // chunk 1 starts at the leading group test (table state 2), chunk 2 is read
+  // in both states and chosen by chunk 1's exit state; nothing follows a
+  // chunk 1 that ended the code
+  uint32_t e1, e2;
+  if constexpr (DIMS == 1) {
+    // a 1D code (4 positions, at most 7 bits with the leading test) fits chunk 1
+    e1 = rd.chunk1_fast(g);
+    e2 = 0;
+  } else {
+    uint32_t e2a, e2b;
+    rd.chunks_fast(g, e1, e2a, e2b);
+    const uint32_t e2s = (e1 & kEntryState) ? e2b : e2a;
+    e2 = keep_if_bit13(e2s, e1);  // nothing after a chunk 1 that ended
+  }
+  return lut_finish<DIMS, PW>(bits, n, rd, slow, nf, m, w, e1, e2);
+}
+
+// The 3D decoder's plane step.  n is kept at most N-1 (with n = N-1 the group
+// part is the last position's bit alone, looked up in two dedicated entries),
+// so the verbatim mask is one shift.  Common case: the code ends within the
+// two chunks, below position N-1 (one wave-uniform test covers both).
 template <int DIMS, typename PW, typename Reader>
 ZFP_HD PW decode_plane_fast(unsigned& bits, unsigned& n, Reader& rd, bool& slow, bool& rare) {
   constexpr unsigned N = 1u << (2 * DIMS);
@@ -1356,27 +1365,28 @@ ZFP_HD PW decode_plane_fast(unsigned& bits, unsigned& n, Reader& rd, bool& slow,
   const uint32_t used = S & kUsedMask;
   const uint32_t ones = ((e1 >> kOnesShift) & kChunkMask) |
                         (((e2 >> kOnesShift) & kChunkMask) << ((e1 >> kPosShift) & 31u));
-  uint64_t ones64 = ones;
-  uint32_t np = npos, take = used;
-  const uint32_t q = N - 1 - nf;
   // One wave-uniform test for both rare cases: a code longer than the two
   // chunks (the sum carries the marker) and one reaching position N-1
   // (nf + npos >= N; nf + npos < 2N).
   slow = false;
   rare = any_lane(and_or(S, kNotEnded, nf + npos) >= N);  // (nf + npos < 2N)
-  if (__builtin_expect(rare, 0)) {
-    const bool implied = npos > q;
-    if (implied) {  // the code reaches position N-1: the one there is implied
-      take = implied_end(e1, e2, q, ones64);  // within the budget (fast_room)
-      np = q + 1u;
-    }
-    slow = !implied && used >= kNotEnded;  // longer than two chunks: decode_plane_lut
-  }
+  // The budget: past its budget a block reads as zeros (it ends there), so a code that ended did so within the
+  // budget or with the zero group test that follows a one read with the
+  // budget's last bit: taken as read, min(used, bits - nf) bits.  A lane with
+  // fewer than nf bits reads zeros for the rest of its verbatim part and a
+  // "0" leading test past its block: a verbatim-only plane, all its bits.  So
+  // the common path only clips the advance at the budget.  A code that did
+  // not end within the two chunks (cut by the budget, or longer than the
+  // chunks) or reaches position N-1 takes, for the whole wave, the
+  // budget-aware resolution from the entries already read (lut_finish);
+  // `slow` is left only for the general decoder's cases.
+  if (__builtin_expect(rare, 0))
+    return lut_finish<DIMS, PW>(bits, n, rd, slow, nf, umin(nf, bits), w, e1, e2);
   // bits >= nf of the plane from the group code, below it verbatim: one
   // v_bfi_b32 a dword under the mask ~0 << nf
-  const PW x = merge_at<PW>(nf, ones64, w);
-  n = nf + np;
-  const unsigned adv = nf + take;
+  const PW x = merge_at<PW>(nf, ones, w);
+  n = nf + npos;
+  const unsigned adv = umin(nf + used, bits);
 #if defined(CUZFP_EXP_DEC_EXTRA_RT)  // timing experiment: one more dependent LDS round trip a plane
   {
     uint32_t a = adv;
@@ -1390,11 +1400,6 @@ ZFP_HD PW decode_plane_fast(unsigned& bits, unsigned& n, Reader& rd, bool& slow,
   bits -= adv;
   return x;
 }
-
-// Budget for two fast steps: 2 x (N-1 verbatim + 21 group bits)
-template <int DIMS> struct fast_room {
-  static constexpr unsigned value = 2u * ((1u << (2 * DIMS)) - 1u + 21u);
-};
 
 // Plane loop: the table decoder for every lane, then, only when some lane of
 // the wave needs it, the general decoder for those lanes.
@@ -1416,8 +1421,13 @@ ZFP_HD PW decode_plane_any(unsigned& bits, unsigned& n, Reader& rd) {
   return x;
 }
 
-// The fast step with its fallbacks (the budget-aware steps) for the lanes
-// that need them.
+// 2D and 3D (1D: the budget-aware step, whose codes fit one chunk; its
+// workgroups load only the chunk-1 tables).  CUZFP_FAST_DIMS=3: 3D only (A/B).
+#ifndef CUZFP_FAST_DIMS
+#define CUZFP_FAST_DIMS 2
+#endif
+// The fast step with the general decoder for the lanes the tables cannot finish
+// (none on the bench fields: tools/dec_paths.cpp).
 template <int DIMS, typename PW, typename Reader>
 ZFP_HD PW decode_plane_fast_any(unsigned& bits, unsigned& n, Reader& rd) {
   const auto pos0 = rd.pos;
@@ -1430,16 +1440,7 @@ ZFP_HD PW decode_plane_fast_any(unsigned& bits, unsigned& n, Reader& rd) {
       rd.init(pos0);
       n = n0;
       bits = bits0;
-      x = decode_plane_lut<DIMS, PW>(bits, n, rd, slow);
-      ZFP_COUNT_PATH(slow ? 3 : 4);
-    }
-    if (__builtin_expect(any_lane(slow), 0)) {
-      if (slow) {
-        rd.init(pos0);
-        n = n0;
-        bits = bits0;
-        x = decode_plane<DIMS, PW>(bits, n, rd);
-      }
+      x = decode_plane<DIMS, PW>(bits, n, rd);
     }
   }
   return x;
@@ -1460,7 +1461,7 @@ ZFP_HD int decode_half(planes<UInt, DIMS>& P, unsigned& bits, unsigned& n, int c
     if constexpr (prio_of<Reader>::value)
       progress_priority<CUZFP_DPRIO_T2, CUZFP_DPRIO_T1, CUZFP_DPRIO_T0>(uniform(c));
     PW xa, xb;
-    if (DIMS == 3 && !any_lane(bits < fast_room<DIMS>::value)) {
+    if constexpr (DIMS >= CUZFP_FAST_DIMS) {
       xa = decode_plane_fast_any<DIMS, PW>(bits, n, rd);
       xb = decode_plane_fast_any<DIMS, PW>(bits, n, rd);
       ZFP_STAMP(4);  // diagnostic builds: the last fast pair's end

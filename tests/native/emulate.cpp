@@ -130,7 +130,7 @@ extern "C" long long emu_fuzz_plane(unsigned long long seed, long long trials, i
       buf[i] = v;
     }
     const unsigned n0 = (unsigned)(rnd() % (N + 1));
-    const unsigned bits0 = 1u + (unsigned)(rnd() % 160);
+    const unsigned bits0 = (unsigned)(rnd() % 161);  // 0: a lane whose block is done (it keeps stepping with its wave)
     const size_t end = bits0;  // the budget ends where the block does
     HostReader ra{buf, 6, 0, end}, rb{buf, 6, 0, end};
     unsigned na = n0, ba = bits0, nb = n0, bb = bits0;
@@ -148,10 +148,11 @@ extern "C" long long emu_fuzz_plane(unsigned long long seed, long long trials, i
     // n = N-1 and n = N are the same state (the table steps keep n <= N-1)
     auto cap = [&](unsigned v) { return v < N - 1 ? v : N - 1; };
     if (xa != xb || cap(na) != cap(nb) || ba != bb || ra.pos != rb.pos) bad++;
-    if (dims == 3 && bits0 >= cuzfp::fast_room<3>::value / 2) {  // the budget-free step (decode_half's fast pairs)
+    if (dims >= 2) {  // the fast step with the budget (decode_half's every 2D/3D step)
       HostReader rc{buf, 6, 0, end};
       unsigned nc = n0, bc = bits0;
-      const uint64_t xc = cuzfp::decode_plane_fast_any<3, uint64_t>(bc, nc, rc);
+      const uint64_t xc = dims == 3 ? cuzfp::decode_plane_fast_any<3, uint64_t>(bc, nc, rc)
+                                    : (uint64_t)cuzfp::decode_plane_fast_any<2, uint32_t>(bc, nc, rc);
       if (xc != xb || cap(nc) != cap(nb) || bc != bb || rc.pos != rb.pos) bad++;
     }
   }

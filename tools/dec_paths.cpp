@@ -34,7 +34,7 @@ int main(int argc, char** argv) {
     HostWriter w{s.data(), b * maxbits, (b + 1) * maxbits};
     cuzfp::encode_block<float, 3>(f, maxbits, w);
   }
-  const char* nm[9] = {"fast ok", "fast rare, ok", "fast -> table", "table -> general", "table ok",
+  const char* nm[9] = {"fast ok", "fast rare (table)", "fast -> general", "-", "-",
                        "table ok", "table -> general", "-", "-"};
   long lane[9] = {0}, wave[9] = {0};
   double wave_calls = 0;
