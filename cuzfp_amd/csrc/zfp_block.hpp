@@ -1357,9 +1357,15 @@ ZFP_HD PW decode_plane_fast(unsigned& bits, unsigned& n, Reader& rd, bool& slow,
   uint64_t w;
   uint32_t g;
   rd.windows(nf, w, g);
-  uint32_t e1, e2a, e2b;
-  rd.chunks_fast(g, e1, e2a, e2b);
-  const uint32_t e2 = keep_if_bit13((e1 & kEntryState) ? e2b : e2a, e1);
+  uint32_t e1, e2;
+  if constexpr (DIMS == 1) {
+    e1 = rd.chunk1_fast(g);  // a 1D code fits chunk 1
+    e2 = 0;
+  } else {
+    uint32_t e2a, e2b;
+    rd.chunks_fast(g, e1, e2a, e2b);
+    e2 = keep_if_bit13((e1 & kEntryState) ? e2b : e2a, e1);
+  }
   const uint32_t S = e1 + e2;
   const uint32_t npos = S >> kPosShift & 31u;
   const uint32_t used = S & kUsedMask;
@@ -1421,10 +1427,10 @@ ZFP_HD PW decode_plane_any(unsigned& bits, unsigned& n, Reader& rd) {
   return x;
 }
 
-// 2D and 3D (1D: the budget-aware step, whose codes fit one chunk; its
-// workgroups load only the chunk-1 tables).  CUZFP_FAST_DIMS=3: 3D only (A/B).
+// Every dimensionality (1D reads chunk 1 only).  CUZFP_FAST_DIMS=2/3: the
+// budget-aware step below that (A/B builds).
 #ifndef CUZFP_FAST_DIMS
-#define CUZFP_FAST_DIMS 2
+#define CUZFP_FAST_DIMS 1
 #endif
 // The fast step with the general decoder for the lanes the tables cannot finish
 // (none on the bench fields: tools/dec_paths.cpp).

@@ -148,11 +148,12 @@ extern "C" long long emu_fuzz_plane(unsigned long long seed, long long trials, i
     // n = N-1 and n = N are the same state (the table steps keep n <= N-1)
     auto cap = [&](unsigned v) { return v < N - 1 ? v : N - 1; };
     if (xa != xb || cap(na) != cap(nb) || ba != bb || ra.pos != rb.pos) bad++;
-    if (dims >= 2) {  // the fast step with the budget (decode_half's every 2D/3D step)
+    {  // the fast step with the budget (decode_half's every step)
       HostReader rc{buf, 6, 0, end};
       unsigned nc = n0, bc = bits0;
       const uint64_t xc = dims == 3 ? cuzfp::decode_plane_fast_any<3, uint64_t>(bc, nc, rc)
-                                    : (uint64_t)cuzfp::decode_plane_fast_any<2, uint32_t>(bc, nc, rc);
+                          : dims == 2 ? (uint64_t)cuzfp::decode_plane_fast_any<2, uint32_t>(bc, nc, rc)
+                                      : (uint64_t)cuzfp::decode_plane_fast_any<1, uint32_t>(bc, nc, rc);
       if (xc != xb || cap(nc) != cap(nb) || bc != bb || rc.pos != rb.pos) bad++;
     }
   }
