@@ -1486,6 +1486,33 @@ ZFP_HD int decode_half(planes<UInt, DIMS>& P, unsigned& bits, unsigned& n, int c
   return c;
 }
 
+// decode_half with compile-time plane numbers (32-bit halves whose every lane
+// decodes down to plane 0, the common case): each plane is a fixed register
+// (no VGPR-relative or compare-select writes of a runtime plane number) and
+// the priority drops sit at fixed trips.  Returns the highest plane left
+// unset (-1: none), as decode_half.
+template <int H, int C, typename UInt, int DIMS, typename Reader>
+ZFP_HD int decode_half_fixed(planes<UInt, DIMS>& P, unsigned& bits, unsigned& n, Reader& rd) {
+  typedef typename plane_word<DIMS>::type PW;
+  if constexpr (C >= 1) {
+    if (!any_lane(bits != 0)) return C;
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(CUZFP_NO_PRIO)
+    if constexpr (prio_of<Reader>::value) {
+      if constexpr (C == CUZFP_DPRIO_T2) __builtin_amdgcn_s_setprio(2);
+      else if constexpr (C == CUZFP_DPRIO_T1) __builtin_amdgcn_s_setprio(1);
+      else if constexpr (C == CUZFP_DPRIO_T0) __builtin_amdgcn_s_setprio(0);
+    }
+#endif
+    const PW xa = decode_plane_fast_any<DIMS, PW>(bits, n, rd);
+    const PW xb = decode_plane_fast_any<DIMS, PW>(bits, n, rd);
+    ZFP_STAMP(4);  // diagnostic builds: the last pair's end
+    P.template set<H>(C, xa);
+    P.template set<H>(C - 1, xb);
+    return decode_half_fixed<H, C - 2>(P, bits, n, rd);
+  }
+  return C;
+}
+
 // Planes left unset by the loop must read as zero.  In 3D (set() assigns a
 // whole plane) only those are zeroed, after the loop; zeroing the whole array
 // before it costs ~90 moves a wave (the compiler then also shuffles the array
@@ -1509,6 +1536,14 @@ ZFP_HD void decode_planes(planes<UInt, DIMS>& P, unsigned budget, unsigned maxpr
   const int kmin = PREC > (int)maxprec ? PREC - (int)maxprec : 0;
   unsigned bits = budget, n = 0;
   if constexpr (!(kLazyZero && DIMS == 3)) P.zero();
+#if !defined(CUZFP_DEC_LOOP)  // (CUZFP_DEC_LOOP: the rolled loop for every block, A/B builds)
+  if constexpr (PREC == 32 && DIMS >= CUZFP_FAST_DIMS) {
+    if (!any_lane(kmin != 0)) {  // every lane decodes down to plane 0 (normal floats)
+      zero_planes<0>(P, decode_half_fixed<0, 31>(P, bits, n, rd));
+      return;
+    }
+  }
+#endif
   if constexpr (PREC == 64) {
     zero_planes<1>(P, decode_half<1>(P, bits, n, kmin > 32 ? kmin - 32 : 0, rd));
     if (kmin >= 32) {
