@@ -18,6 +18,7 @@ static float poly(float x) {
   return x + xx * yy;
 }
 
+static long g_wide_r15 = 0, g_wide_len_only = 0;
 int main(int argc, char** argv) {
   const int n = argc > 1 ? atoi(argv[1]) : 256;
   const int rough = argc > 2 ? atoi(argv[2]) : 0;
@@ -38,7 +39,7 @@ int main(int argc, char** argv) {
   const size_t nwaves = (blocks + 63) / 64;
   for (size_t w = 0; w < nwaves; w++) {
     int wsteps = 0;
-    bool act[64][32] = {}, rz[64][32] = {}, wide[64][32] = {}, full[64][32] = {}, fit[64][32] = {};
+    bool act[64][32] = {}, rz[64][32] = {}, wide[64][32] = {}, full[64][32] = {}, fit[64][32] = {}, r15[64][32] = {};
     unsigned glen[64][32] = {};
     for (int l = 0; l < 64; l++) {
       const size_t b = w * 64 + l;
@@ -73,6 +74,7 @@ int main(int argc, char** argv) {
         act[l][k] = true;
         rz[l][k] = r == 0;
         wide[l][k] = (r >> 16) != 0;
+        r15[l][k] = (r >> 15) != 0;
         full[l][k] = nn == 64;
         // plane code length (unbudgeted)
         unsigned len = nn;
@@ -107,6 +109,9 @@ int main(int argc, char** argv) {
       fprintf(wf, "%d\n", wsteps);
     }
     for (int k = 0; k < wsteps; k++) {
+      bool any15 = false, anylong = false;
+      for (int l = 0; l < 64; l++) if (act[l][k]) { any15 |= r15[l][k]; anylong |= !fit[l][k]; }
+      g_wide_r15 += any15; g_wide_len_only += !any15 && anylong;
       bool all0 = true, anyw = false, allf = true, allfit = true;
       unsigned gmax = 0;
       for (int l = 0; l < 64; l++) {
@@ -132,6 +137,7 @@ int main(int argc, char** argv) {
       wave_g60[k] += gmax > 60;
     }
   }
+  printf("wide wave-steps per wave: some lane r >= 2^15 %.2f, only len > 64 %.2f\n", (double)g_wide_r15 / nwaves, (double)g_wide_len_only / nwaves);
   printf("blocks %zu waves %zu: planes per block mean %.2f, wave steps mean %.2f\n", blocks, nwaves,
          (double)sum_planes / blocks, (double)sum_wave_steps / nwaves);
   printf("step lanes_act%%  r==0%%  n==64%%  r>=2^16%% | waves: steps  all_r0%%  any_wide%%  all_full%%  all_fit64%%  grp>20%% grp>40%% grp>60%%\n");
