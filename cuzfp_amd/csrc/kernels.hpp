@@ -696,7 +696,7 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
           L[j * 64] = __builtin_amdgcn_alignbit(nxt, prev, s0);
           prev = nxt;
         }
-        // the block reads as zeros past its last bit (decode_plane_lut relies on it)
+        // the block reads as zeros past its last bit (the plane steps rely on it)
         if (g.maxbits & 31) L[(D - 1) * 64] &= (1u << (g.maxbits & 31)) - 1u;
       }
     }
