@@ -3,6 +3,12 @@
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...     (one process per GPU)
 
+With --gpus N > 1 and no launcher around it (WORLD_SIZE unset), bench.py
+starts its N ranks itself through torch.distributed.run before touching the
+GPU; a WORLD_SIZE that differs from --gpus is an error, so a run never
+reports fewer ranks than it was asked for.  The line records what the ranks
+saw (world_size_seen, backend, device_count, rank_devices).
+
 A step is one pass of the hot path over one batch: encode the rank's array
 into its fixed-rate stream, then decode the stream back, both on the GPU with
 the data already in HBM.  Workload (BASELINE.json configs[1]): a 256^3 float32
@@ -75,7 +81,94 @@ def parse():
     p.add_argument("--config5-edge", type=int, default=1024, help="edge of configs[4]'s global array")
     p.add_argument("--config5-steps", type=int, default=10)
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    p.add_argument("--dry-run-cpu", action="store_true",
+                   help="test mode, no GPU: every rank runs the gloo backend and the CPU oracle stands in for "
+                        "the codec, so the launcher and the rank bookkeeping can be checked on a CPU-only host; "
+                        "the line it prints is not a measurement")
     return p.parse_args()
+
+
+def launch_ranks(args) -> int:
+    """--gpus N > 1 without a launcher: start N ranks of this script with
+    torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1) and
+    return their exit code.  Runs before anything touches the GPU, and starts
+    the ranks as children (no exec), so `python bench.py --gpus 8` measures 8
+    ranks or fails -- it can never report one."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, CUZFP_BENCH_LAUNCHED="1")
+    return subprocess.call(cmd, env=env)
+
+
+def rank_info(dist, world: int, dev, backend: str) -> dict:
+    """What the ranks saw: the process group's size and backend, the devices
+    this process can see, and every rank's device id (gathered)."""
+    import torch
+    seen = dist.get_world_size() if dist.is_initialized() else 1
+    did = dev.index if dev.type == "cuda" else -1
+    if dist.is_initialized() and seen > 1:
+        t = torch.tensor([did], dtype=torch.int64, device=dev)
+        out = torch.empty(seen, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(out, t)
+        devs = [int(v) for v in out.cpu()]
+    else:
+        devs = [did]
+    return {"world_size_seen": seen, "backend": backend, "device_count": torch.cuda.device_count(),
+            "rank_devices": devs}
+
+
+def dry_run(args):
+    """The launcher and rank bookkeeping of main() on CPUs (gloo), with the
+    CPU oracle standing in for the codec on a small array: tests/test_bench_launch.py
+    checks that `bench.py --gpus 2 --dry-run-cpu` reports two ranks."""
+    import torch
+    import torch.distributed as dist
+    import oracle
+    from cuzfp_amd.datagen import polynomial_slab
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    if oracle.restatement is None:
+        oracle.build(with_reference=False)
+        oracle.reload()
+    n = 16
+    a = polynomial_slab((n * world, n, n), rank * n, (rank + 1) * n, np.float32)
+    mb = int(oracle.restatement.rate_to_maxbits(args.rate, np.float32, 3))
+    dev = torch.device("cpu")
+
+    def step():
+        w = oracle.restatement.compress(a, mb)
+        return oracle.restatement.decompress(w, a.shape, np.float32, mb)
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if world > 1:
+        dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    info = rank_info(dist, world, dev, "gloo" if world > 1 else "none")
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": round(a.nbytes * world * args.steps / float(t) / 1e9, 6),
+                          "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "data": "dry run: CPU oracle on a 16^3 slab per rank, not a measurement",
+                          **info}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def cpu_share() -> tuple[int, int]:
@@ -266,8 +359,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    if world != args.gpus:  # a measurement of fewer ranks than asked for is never printed
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}: launch N ranks (python bench.py --gpus N "
+                         f"starts them itself) or pass --gpus {world}")
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
@@ -464,6 +558,7 @@ def main():
         except Exception:
             traffic = None
 
+    ranks = rank_info(dist, world, dev, "nccl (RCCL)" if world > 1 else "none")
     result = None
     if rank == 0:
         host_path = None
@@ -549,6 +644,7 @@ def main():
             "config5": config5,
             "max_abs_err": max_err,
             "parity": parity,
+            **ranks,
         }
         print(json.dumps(result), flush=True)
     if world > 1:
@@ -558,4 +654,10 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    _args = parse()
+    if _args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(_args))
+    if _args.dry_run_cpu:
+        dry_run(_args)
+    else:
+        main()

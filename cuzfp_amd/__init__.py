@@ -83,6 +83,8 @@ def library() -> ctypes.CDLL:
     lib.cuzfp_hip_decompress_host.argtypes = [vp, sz, i, u, u, u, u, vp, i]
     lib.cuzfp_hip_copy.restype = i
     lib.cuzfp_hip_copy.argtypes = [vp, vp, sz, vp]
+    lib.cuzfp_hip_release_host_cache.restype = i
+    lib.cuzfp_hip_release_host_cache.argtypes = [i]
     _lib = lib
     return lib
 
@@ -172,7 +174,15 @@ def encode(x, maxbits: int, out=None, stream=None):
     if not x.is_cuda:
         raise ValueError("encode: expects a device tensor (use compress_host for host arrays)")
     if _broadcast(x):
-        x = x.contiguous()  # materialise a broadcast view (a zero stride means "contiguous" to the C-ABI)
+        # materialise a broadcast view (a zero stride means "contiguous" to the
+        # C-ABI) on the launch stream, after the work already queued on torch's
+        # current stream, and keep the copy alive until the kernel that reads
+        # it has run (record_stream: the caching allocator waits for that stream)
+        s = torch.cuda.current_stream(x.device) if stream is None else stream
+        s.wait_stream(torch.cuda.current_stream(x.device))
+        with torch.cuda.stream(s):
+            x = x.contiguous()
+        x.record_stream(s)
     t = type_code(x.dtype)
     nx, ny, nz = _extents(x.shape)
     nbytes = stream_bytes(x.shape, x.dtype, maxbits)
@@ -209,6 +219,9 @@ def decode(words, shape, dtype, maxbits: int, out=None, stream=None):
 def copy(src, dst, stream=None):
     """Device-to-device copy through cuzfp_hip_copy (16-byte non-temporal
     accesses): the bandwidth calibrator bench.py reports beside the codec."""
+    for name, t in (("src", src), ("dst", dst)):
+        if not t.is_cuda or not t.is_contiguous():
+            raise ValueError(f"copy: {name} must be a contiguous device tensor")
     nbytes = src.numel() * src.element_size()
     if dst.numel() * dst.element_size() < nbytes:
         raise ValueError("copy: destination too small")
@@ -232,6 +245,12 @@ def compress_host(a: np.ndarray, maxbits: int, nstreams: int = 4, out: np.ndarra
                                            out.ctypes.data, out.nbytes, ctypes.byref(got), nstreams)
     _check("compress_host", rc)
     return out
+
+
+def release_host_cache(device: int = -1) -> None:
+    """Free the host pipeline's retained device buffers, pinned staging buffers,
+    streams and events (cuzfp_hip_release_host_cache; -1 = the current device)."""
+    _check("release_host_cache", library().cuzfp_hip_release_host_cache(device))
 
 
 def decompress_host(words: np.ndarray, shape, dtype, maxbits: int, nstreams: int = 4,

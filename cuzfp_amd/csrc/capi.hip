@@ -20,11 +20,12 @@ static int make_problem(int type, unsigned nx, unsigned ny, unsigned nz, long lo
   if (!nx || (nz && !ny)) return CUZFP_ERROR_INVALID_ARGUMENT;
   const unsigned dims = nz ? 3 : ny ? 2 : 1;
   const unsigned ebits = type == CUZFP_TYPE_FLOAT ? 9 : type == CUZFP_TYPE_DOUBLE ? 12 : 1;
-  // One wave's LDS image must fit a workgroup's 64 KiB beside the tables: the
-  // decoder's (maxbits / 32 + 5 rows of 256 B + 12 KiB of chunk tables) up to
-  // maxbits 6,464.  CUZFP_MAX_BITS (6,144) is well above the most bits any
-  // block can use (zfp's ZFP_MAX_BITS, 4,171: 3D double at full precision);
-  // past that a stream is padding.
+  // One wave's LDS image must fit a workgroup's LDS beside the tables: the
+  // decoder's (maxbits / 32 + 5 rows of 256 B + 12 KiB of chunk tables) takes
+  // 141 KiB at CUZFP_MAX_BITS (16,384) of gfx950's 160 KiB (the launchers
+  // check the device's budget).  The cap is far above the most bits any block
+  // can use (zfp's ZFP_MAX_BITS, 4,171: 3D double at full precision); past
+  // that a stream is padding.
   if (maxbits < ebits || maxbits > CUZFP_MAX_BITS) return CUZFP_ERROR_INVALID_ARGUMENT;
   Geometry& g = pr->g;
   g.nx = nx;
@@ -130,25 +131,33 @@ struct Chunk {
 };
 
 // The pipeline's device buffers, streams, events and pinned staging ring,
-// kept between calls (per device, one call at a time): allocating and freeing
-// them per call cost about as much as the transfers of a 64 MiB array.
-// Buffers grow to the largest call seen up to kCacheLimit bytes; larger calls
-// use buffers of their own, freed on return.
+// kept between calls (per device; one call at a time per device, calls on
+// different devices run concurrently): allocating and freeing them per call
+// cost about as much as the transfers of a 64 MiB array.  Device buffers grow
+// to the largest call seen up to kCacheLimit bytes (larger calls use buffers
+// of their own, freed on return); the pinned staging buffers are chunk-sized
+// (chunk_bytes(), capped at kPinCacheLimit each; larger chunks stage through
+// buffers freed on return).  cuzfp_hip_release_host_cache() frees a device's
+// cache (include/cuzfp_hip.h documents the retention).
 constexpr size_t kCacheLimit = 1ull << 30;
+constexpr size_t kPinCacheLimit = 64ull << 20;
 constexpr int kMaxStreams = 8;
 
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
-  bool owned_by_call = false;
   hipError_t get(size_t bytes) {  // at least `bytes`, contents undefined
     if (bytes <= cap) return hipSuccess;
-    if (p && !owned_by_call) (void)hipFree(p);
-    p = nullptr;
-    cap = 0;
+    release();
     const hipError_t e = hipMalloc(&p, std::max<size_t>(bytes, 16));
     if (e == hipSuccess) cap = bytes;
+    else p = nullptr;
     return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
   }
 };
 
@@ -157,17 +166,42 @@ struct HostBuf {
   size_t cap = 0;
   hipError_t get(size_t bytes) {
     if (bytes <= cap) return hipSuccess;
+    release();
+    const hipError_t e = hipHostMalloc(&p, std::max<size_t>(bytes, 16), hipHostMallocDefault);
+    if (e == hipSuccess) cap = bytes;
+    else p = nullptr;
+    return e;
+  }
+  void release() {
     if (p) (void)hipHostFree(p);
     p = nullptr;
     cap = 0;
-    const hipError_t e = hipHostMalloc(&p, std::max<size_t>(bytes, 16), hipHostMallocDefault);
-    if (e == hipSuccess) cap = bytes;
+  }
+};
+
+// a pinned staging buffer for one call: the cache's up to kPinCacheLimit,
+// else the call's own (freed on return)
+struct CallHostBuf {
+  void* p = nullptr;
+  bool own = false;
+  ~CallHostBuf() {
+    if (own && p) (void)hipHostFree(p);
+  }
+  hipError_t get(HostBuf& cached, size_t bytes) {
+    if (bytes <= kPinCacheLimit) {
+      const hipError_t e = cached.get(bytes);
+      p = cached.p;
+      return e;
+    }
+    own = true;
+    const hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+    if (e != hipSuccess) p = nullptr;
     return e;
   }
 };
 
 struct PipelineCache {
-  int device = -1;
+  std::mutex mu;  // one call at a time on this device
   DevBuf d_data, d_stream;
   hipStream_t st[kMaxStreams] = {};
   hipEvent_t ev_in[kMaxStreams] = {}, ev_kernel[kMaxStreams] = {}, ev_done[kMaxStreams] = {};
@@ -175,8 +209,8 @@ struct PipelineCache {
   int nst = 0;
 };
 
-std::mutex g_pipeline_mu;
-PipelineCache g_pipeline[16];  // by device ordinal; intentionally never freed (process lifetime)
+// by device ordinal; kept for the process lifetime unless released
+PipelineCache g_pipeline[kMaxDevices];
 
 // device buffers for one call: the cache's, or the call's own past kCacheLimit
 struct CallBuf {
@@ -253,9 +287,9 @@ static int host_pipeline(const Problem& p, bool encode, void* h_data, void* h_st
   const bool stream_pinned = is_pinned_host(h_stream);
   int dev = 0;
   CUZFP_HIP_TRY(hipGetDevice(&dev));
-  if (dev < 0 || dev >= 16) return CUZFP_ERROR_INVALID_ARGUMENT;
-  std::lock_guard<std::mutex> lock(g_pipeline_mu);
+  if (dev < 0 || dev >= kMaxDevices) return CUZFP_ERROR_INVALID_ARGUMENT;
   PipelineCache& r = g_pipeline[dev];
+  std::lock_guard<std::mutex> lock(r.mu);
   CallBuf bd, bs;
   CUZFP_HIP_TRY(bd.get(r.d_data, data_bytes));
   CUZFP_HIP_TRY(bs.get(r.d_stream, sbytes));
@@ -273,9 +307,10 @@ static int host_pipeline(const Problem& p, bool encode, void* h_data, void* h_st
     CUZFP_HIP_TRY(hipEventCreateWithFlags(&r.ev_done[i], hipEventDisableTiming));
     r.nst = i + 1;
   }
+  CallHostBuf pin_in[kMaxStreams], pin_out[kMaxStreams];
   for (int i = 0; i < S; i++) {
-    if (!in_pinned) CUZFP_HIP_TRY(r.pin_in[i].get(max_in));
-    if (!out_pinned) CUZFP_HIP_TRY(r.pin_out[i].get(max_out));
+    if (!in_pinned) CUZFP_HIP_TRY(pin_in[i].get(r.pin_in[i], max_in));
+    if (!out_pinned) CUZFP_HIP_TRY(pin_out[i].get(r.pin_out[i], max_out));
   }
   // on every return (an error included) nothing of this call is left running
   // on the cached streams when the next call reuses them (declared after the
@@ -305,7 +340,7 @@ static int host_pipeline(const Problem& p, bool encode, void* h_data, void* h_st
       if (!out_pinned) {
         size_t o0, o1;
         out_range(chunks[j], &o0, &o1);
-        if (o1 > o0) std::memcpy((encode ? hs : hd) + o0, r.pin_out[sj].p, o1 - o0);
+        if (o1 > o0) std::memcpy((encode ? hs : hd) + o0, pin_out[sj].p, o1 - o0);
       }
     }
     if (i >= n) continue;
@@ -318,8 +353,8 @@ static int host_pipeline(const Problem& p, bool encode, void* h_data, void* h_st
     char* dst = (encode ? dd : ds) + i0;
     if (i1 > i0) {
       if (!in_pinned) {
-        std::memcpy(r.pin_in[s].p, src, i1 - i0);
-        src = (char*)r.pin_in[s].p;
+        std::memcpy(pin_in[s].p, src, i1 - i0);
+        src = (char*)pin_in[s].p;
       }
       CUZFP_HIP_TRY(hipMemcpyAsync(dst, src, i1 - i0, hipMemcpyHostToDevice, st));
     }
@@ -340,7 +375,7 @@ static int host_pipeline(const Problem& p, bool encode, void* h_data, void* h_st
     out_range(c, &o0, &o1);
     if (o1 > o0) {
       char* osrc = (encode ? ds : dd) + o0;
-      char* odst = out_pinned ? (encode ? hs : hd) + o0 : (char*)r.pin_out[s].p;
+      char* odst = out_pinned ? (encode ? hs : hd) + o0 : (char*)pin_out[s].p;
       CUZFP_HIP_TRY(hipMemcpyAsync(odst, osrc, o1 - o0, hipMemcpyDeviceToHost, st));
     }
     CUZFP_HIP_TRY(hipEventRecord(r.ev_done[s], st));
@@ -447,7 +482,10 @@ int cuzfp_hip_copy(const void* d_src, void* d_dst, size_t bytes, hipStream_t str
     return CUZFP_ERROR_INVALID_ARGUMENT;
   if (!bytes) return CUZFP_SUCCESS;
   const size_t n16 = bytes / 16;
-  const unsigned grid = (unsigned)std::min<size_t>((n16 + 255) / 256, 1u << 30);
+  // one grid over the buffer up to 16 Mi workgroups (the measured shape, 4 GiB
+  // a launch); past that the kernel's grid-stride loop covers the rest, so a
+  // launch never nears the 2^32 work-item limit
+  const unsigned grid = (unsigned)std::min<size_t>((n16 + 255) / 256, 1u << 24);
   hipLaunchKernelGGL(copy16_nt, dim3(grid), dim3(256), 0, stream, (const u32x4*)d_src, (u32x4*)d_dst, n16);
   const hipError_t e = hipGetLastError();
   t_last_hip = e;
@@ -466,6 +504,34 @@ int cuzfp_hip_compress_host(const void* h_data, int type, unsigned nx, unsigned 
   rc = host_pipeline(p, true, (void*)h_data, h_stream, nstreams);
   if (!rc && out_bytes) *out_bytes = need;
   return rc;
+}
+
+int cuzfp_hip_release_host_cache(int device) {
+  if (device < -1 || device >= kMaxDevices) return CUZFP_ERROR_INVALID_ARGUMENT;
+  if (device == -1) CUZFP_HIP_TRY(hipGetDevice(&device));
+  if (device < 0 || device >= kMaxDevices) return CUZFP_ERROR_INVALID_ARGUMENT;
+  PipelineCache& r = g_pipeline[device];
+  std::lock_guard<std::mutex> lock(r.mu);
+  if (!r.nst && !r.d_data.p && !r.d_stream.p) return CUZFP_SUCCESS;  // never used
+  int prev = 0;
+  CUZFP_HIP_TRY(hipGetDevice(&prev));
+  CUZFP_HIP_TRY(hipSetDevice(device));
+  for (int i = 0; i < r.nst; i++) (void)hipStreamSynchronize(r.st[i]);
+  r.d_data.release();
+  r.d_stream.release();
+  for (int i = 0; i < kMaxStreams; i++) {
+    r.pin_in[i].release();
+    r.pin_out[i].release();
+  }
+  for (int i = 0; i < r.nst; i++) {
+    (void)hipEventDestroy(r.ev_in[i]);
+    (void)hipEventDestroy(r.ev_kernel[i]);
+    (void)hipEventDestroy(r.ev_done[i]);
+    (void)hipStreamDestroy(r.st[i]);
+  }
+  r.nst = 0;
+  CUZFP_HIP_TRY(hipSetDevice(prev));
+  return CUZFP_SUCCESS;
 }
 
 int cuzfp_hip_decompress_host(const void* h_stream, size_t stream_bytes, int type,

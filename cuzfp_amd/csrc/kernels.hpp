@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
+#include <atomic>
+
 #if defined(CUZFP_PROBE) && CUZFP_PROBE == 9
 // Diagnostic build (tools/probe.py stamps): lane 0 of every wave records
 // s_memtime at the codec's phase boundaries, plus its HW_ID / XCC_ID.
@@ -560,11 +562,36 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS, t
   Scalar f[N];
 #if defined(CUZFP_EXP_NOLOAD)  // timing experiment (tools/variants.py): a synthetic smooth block, no HBM reads
   for (int i = 0; i < N; i++) f[i] = (Scalar)(1.0f + 0.001f * (float)((b & 255) + 3 * i + (i >> 2) * (i & 3)));
+#elif defined(CUZFP_EXP_GENLOAD)  // timing experiment (tools/xvar.py): the bench's polynomial field computed
+  // in the kernel with the generator's IEEE operations (cuzfp_amd/datagen.py), so the
+  // block's values -- and the stream -- are the bench's, without HBM reads
+  if (b < g.nblocks) {
+    const BlockPos bp = block_pos<DIMS>(g, b);
+    auto axis = [](uint32_t i, uint32_t n) {
+      const float x = __fdiv_rn((float)(int)(2 * i - n + 1), (float)n);
+      const float xx = __fmul_rn(x, x);
+      const float yy = __fsub_rn(__fmul_rn(xx, 4.0f), 3.0f);
+      return __fadd_rn(x, __fmul_rn(xx, yy));
+    };
+    for (int z = 0; z < 4; z++)
+      for (int y = 0; y < 4; y++)
+        for (int x = 0; x < 4; x++)
+          f[16 * z + 4 * y + x] = (Scalar)__fmul_rn(__fmul_rn(axis(4 * bp.ix + x, g.nx), axis(4 * bp.iy + y, g.ny)),
+                                                    axis(4 * bp.iz + z, g.nz));
+#if defined(CUZFP_EXP_GENBOTH)  // ... and the real gathers too, each value + 0 * its loaded twin
+    Scalar h[N];
+    gather<Scalar, DIMS, FAST>(data, g, bp, h);
+    for (int i = 0; i < N; i++) f[i] = f[i] + h[i] * (Scalar)0;
+#endif
+  }
 #else
   if (b < g.nblocks) gather<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
 #endif
 #pragma unroll
   for (uint32_t i = 0; i < kTabPieces / kLanes; i++) ((uint4*)stab)[lane + i * kLanes] = tab16[i];
+#if defined(CUZFP_EXP_PAD) && defined(__HIP_DEVICE_COMPILE__) && CUZFP_EXP_PAD_AT == 0
+  exp_pad(lane);  // timing experiment: dummy VALU work while the gathers are in flight
+#endif
   if (b < g.nblocks) {
     if constexpr (ALIGNED) {
       uint64_t* mine = lds + lane;
@@ -753,10 +780,31 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
 // ---------------------------------------------------------------------------
 // Launchers
 
-// waves per workgroup: as many as fit a workgroup's 64 KiB of LDS (up to 4)
+// The current device's LDS budget of one workgroup
+// (hipDeviceAttributeMaxSharedMemoryPerBlock: 160 KiB on MI355X, where a single
+// workgroup may use the whole CU's LDS), read once per device; 64 KiB if the
+// runtime cannot say.  Thread-safe: each device's slot is an atomic written
+// with the same value by whichever thread reads it first.
+static inline size_t lds_cap_bytes() {
+  static std::atomic<int> cap[kMaxDevices];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return 65536;
+  int c = cap[dev].load(std::memory_order_relaxed);
+  if (!c) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess || n <= 0)
+      n = 65536;
+    cap[dev].store(n, std::memory_order_relaxed);
+    c = n;
+  }
+  return (size_t)c;
+}
+
+// waves per workgroup: as many as fit a workgroup's LDS budget (up to 4)
 static inline uint32_t waves_per_group(uint32_t lds_words, size_t shared_bytes = 0) {
+  const size_t cap = lds_cap_bytes();
   uint32_t w = kWavesPerGroup;
-  while (w > 1 && (size_t)w * lds_words * 8 + shared_bytes > 65536) w >>= 1;
+  while (w > 1 && (size_t)w * lds_words * 8 + shared_bytes > cap) w >>= 1;
   return w;
 }
 
@@ -767,21 +815,26 @@ static inline uint32_t waves_per_group(uint32_t lds_words, size_t shared_bytes =
 // 320^3 (1.95 rounds) the decoder still gains (57.5 vs 61.0 us) and the
 // encoder no longer does (62.8 vs 61.3 us); from 384^3 (3.4 rounds) both lose,
 // 768^3 by 14 % of the step.  CUZFP_PRIO=0/1 in the environment forces either.
+// The environment is read once per process (a function-local static: thread-safe
+// initialisation); the CU count once per device, as lds_cap_bytes.
 static inline bool use_priority(uint32_t nwaves, int waves_per_simd, uint32_t rounds) {
-  static int forced = -2, cus = 0;
-  if (forced == -2) {
+  static const int forced = [] {
     const char* e = getenv("CUZFP_PRIO");
-    forced = (e && *e) ? (atoi(e) != 0) : -1;
-  }
+    return (e && *e) ? (atoi(e) != 0 ? 1 : 0) : -1;
+  }();
   if (forced >= 0) return forced != 0;
-  if (!cus) {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;  // MI355X
-    cus = n;
+  static std::atomic<int> cus[kMaxDevices];
+  int dev = 0, c = 256;  // MI355X
+  if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < kMaxDevices) {
+    c = cus[dev].load(std::memory_order_relaxed);
+    if (!c) {
+      int n = 0;
+      if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+      cus[dev].store(n, std::memory_order_relaxed);
+      c = n;
+    }
   }
-  return nwaves <= (uint32_t)cus * 4u * (uint32_t)waves_per_simd * rounds;
+  return nwaves <= (uint32_t)c * 4u * (uint32_t)waves_per_simd * rounds;
 }
 
 template <typename Scalar, int DIMS>
@@ -793,8 +846,8 @@ int launch_encode_t(const void* data, const Geometry& g, bool fast, uint64_t* st
   gg.vec_io = (g.maxbits % 2 == 0) && ((uintptr_t)stream % 16 == 0);
   gg.lds_words = g.maxbits + kLanes * kSlackWords;  // + per-lane slack
   // the word-aligned writer pads each lane with slack words; very large maxbits
-  // (whose padded image would pass 64 KiB of LDS) take the general writer
-  const bool aligned = (g.maxbits & 63) == 0 && gg.lds_words * 8 + kSpreadTabBytes <= 65536;
+  // (whose padded image would pass the workgroup's LDS) take the general writer
+  const bool aligned = (g.maxbits & 63) == 0 && gg.lds_words * 8 + kSpreadTabBytes <= lds_cap_bytes();
   if (!aligned) gg.lds_words = g.maxbits + 2;
   // (the spread tables are the kernel's static LDS, kSpreadTabBytes a workgroup)
   const uint32_t wpg = waves_per_group(gg.lds_words, kSpreadTabBytes);
@@ -805,12 +858,17 @@ int launch_encode_t(const void* data, const Geometry& g, bool fast, uint64_t* st
     hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, true, true, false>), grid, block, lds, st, d, gg, stream);
   else if (fast && aligned)
     hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, true, true>), grid, block, lds, st, d, gg, stream);
+#if defined(CUZFP_EXP_ONLY3D)
+  else
+    return CUZFP_ERROR_UNSUPPORTED_TYPE;
+#else
   else if (fast)
     hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, true, false>), grid, block, lds, st, d, gg, stream);
   else if (aligned)
     hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, false, true>), grid, block, lds, st, d, gg, stream);
   else
     hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, false, false>), grid, block, lds, st, d, gg, stream);
+#endif
   const hipError_t e = hipGetLastError();
   t_last_hip = e;
   return e == hipSuccess ? CUZFP_SUCCESS : CUZFP_ERROR_HIP;
@@ -851,15 +909,40 @@ int launch_decode_t(const uint64_t* stream, const Geometry& g, bool fast, void* 
     hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, true, false>), grid, block, lds, st, stream, gg, d);
   else if (fast)
     hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, true>), grid, block, lds, st, stream, gg, d);
+#if !defined(CUZFP_EXP_ONLY3D)
   else
     hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, false>), grid, block, lds, st, stream, gg, d);
+#endif
   const hipError_t e = hipGetLastError();
   t_last_hip = e;
   return e == hipSuccess ? CUZFP_SUCCESS : CUZFP_ERROR_HIP;
 }
 
 
-// Per-type entry points (declared in launch.hpp).
+// Per-type entry points (declared in launch.hpp).  Experiment builds
+// (tools/xvar.py, never the product library): CUZFP_EXP_ONLY3D instantiates
+// the 3D fast-gather kernels alone, CUZFP_EXP_STUB no kernel at all, so that
+// a timing variant of the 3D f32 kernels compiles in a fraction of the time.
+#if defined(CUZFP_EXP_ONLY3D) || defined(CUZFP_EXP_STUB)
+template <typename Scalar>
+int launch_encode_type(const Problem& p, const void* data, bool fast, uint64_t* stream,
+                       uint32_t wave0, uint32_t nwaves, hipStream_t st) {
+#if defined(CUZFP_EXP_ONLY3D)
+  if (p.dims == 3 && fast) return launch_encode_t<Scalar, 3>(data, p.g, fast, stream, wave0, nwaves, st);
+#endif
+  (void)p, (void)data, (void)fast, (void)stream, (void)wave0, (void)nwaves, (void)st;
+  return CUZFP_ERROR_UNSUPPORTED_TYPE;
+}
+template <typename Scalar>
+int launch_decode_type(const Problem& p, const uint64_t* stream, bool fast, void* data,
+                       uint32_t wave0, uint32_t nwaves, hipStream_t st) {
+#if defined(CUZFP_EXP_ONLY3D)
+  if (p.dims == 3 && fast) return launch_decode_t<Scalar, 3>(stream, p.g, fast, data, wave0, nwaves, st);
+#endif
+  (void)p, (void)data, (void)fast, (void)stream, (void)wave0, (void)nwaves, (void)st;
+  return CUZFP_ERROR_UNSUPPORTED_TYPE;
+}
+#else
 template <typename Scalar>
 int launch_encode_type(const Problem& p, const void* data, bool fast, uint64_t* stream,
                        uint32_t wave0, uint32_t nwaves, hipStream_t st) {
@@ -879,5 +962,6 @@ int launch_decode_type(const Problem& p, const uint64_t* stream, bool fast, void
     default: return launch_decode_t<Scalar, 3>(stream, p.g, fast, data, wave0, nwaves, st);
   }
 }
+#endif
 
 }  // namespace cuzfp

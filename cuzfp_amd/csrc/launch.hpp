@@ -9,6 +9,7 @@
 namespace cuzfp {
 
 constexpr int kLanes = 64;  // blocks per wave64 (one per lane)
+constexpr int kMaxDevices = 64;  // per-device caches (launch policy, host pipeline)
 
 struct Geometry {
   uint32_t nx, ny, nz;   // array extent (1 for unused dimensions)

@@ -1649,6 +1649,29 @@ __device__ __forceinline__ float absmax_nan(const float* f) {
 }
 #endif
 
+#if defined(CUZFP_EXP_PAD) && defined(__HIP_DEVICE_COMPILE__)
+#ifndef CUZFP_EXP_PAD_AT
+#define CUZFP_EXP_PAD_AT 1
+#endif
+// timing experiment (tools/xvar.py): CUZFP_EXP_PAD x 8 independent dummy VALU
+// ops (v_add_u32, or v_bfi_b32 with CUZFP_EXP_PAD_SLOW), at the gathers
+// (CUZFP_EXP_PAD_AT 0) or after the block's exponent (1, the data is in)
+__device__ __forceinline__ void exp_pad(uint32_t seed) {
+  uint32_t d0 = seed, d1 = seed + 1, d2 = seed + 2, d3 = seed + 3, d4 = seed + 4, d5 = seed + 5, d6 = seed + 6,
+           d7 = seed + 7;
+#if defined(CUZFP_EXP_PAD_SLOW)
+#define ZFP_PAD_OP(r) "v_bfi_b32 " r ", %8, " r ", %9\n"
+#else
+#define ZFP_PAD_OP(r) "v_add_u32 " r ", " r ", %9\n"
+#endif
+  asm volatile(".rept %c10\n" ZFP_PAD_OP("%0") ZFP_PAD_OP("%1") ZFP_PAD_OP("%2") ZFP_PAD_OP("%3")
+               ZFP_PAD_OP("%4") ZFP_PAD_OP("%5") ZFP_PAD_OP("%6") ZFP_PAD_OP("%7") ".endr\n"
+               : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3), "+v"(d4), "+v"(d5), "+v"(d6), "+v"(d7)
+               : "s"(0x0f0f0f0fu), "v"(seed * 3u), "i"(CUZFP_EXP_PAD));
+#undef ZFP_PAD_OP
+}
+#endif
+
 template <typename Scalar, int DIMS, typename Writer>
 ZFP_HD void encode_block(const Scalar* f, unsigned maxbits, Writer& wr) {
   typedef traits<Scalar> T;
@@ -1683,6 +1706,9 @@ ZFP_HD void encode_block(const Scalar* f, unsigned maxbits, Writer& wr) {
     const int emax = fp<Scalar>::template emax<N>((const Scalar*)f);
 #endif
     ZFP_STAMP(1);
+#if defined(CUZFP_EXP_PAD) && defined(__HIP_DEVICE_COMPILE__) && CUZFP_EXP_PAD_AT == 1
+    exp_pad((uint32_t)emax);
+#endif
     maxprec = precision<DIMS>(emax, T::prec);
     const unsigned e = maxprec ? (unsigned)(emax + T::ebias) : 0u;
     if (!e) {  // all-zero block: a single 0 bit, then padding

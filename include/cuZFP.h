@@ -11,7 +11,7 @@
 //   - compress returns the compressed byte count (ceil(blocks*maxbits/64)*8).
 // Differences, all in the direction of CPU zfp 0.5.0 (the reference's own
 // oracle, src/utils/test.py:68-93): non-zero field strides are honoured; any
-// maxbits in [1 + exponent bits, CUZFP_MAX_BITS = 6144] works in every
+// maxbits in [1 + exponent bits, CUZFP_MAX_BITS = 16384] works in every
 // dimensionality (zfp's ZFP_MAX_BITS, the most bits a block can use, is 4171);
 // partial blocks are padded as CPU zfp pads them; failures print one line to
 // stderr and compress returns 0 (the reference prints and continues).

@@ -57,11 +57,14 @@ extern "C" {
 #define CUZFP_TYPE_DOUBLE 4
 
 /* Largest accepted maxbits (bits per block).  Calls with more return
- * CUZFP_ERROR_INVALID_ARGUMENT.  It is above ZFP_MAX_BITS = 4171
+ * CUZFP_ERROR_INVALID_ARGUMENT.  It is far above ZFP_MAX_BITS = 4171
  * (zfp_structs.h:12), the most bits any block can use; beyond that a stream is
- * padding.  The bound keeps one wave's LDS stream image within a workgroup's
- * 64 KiB. */
-#define CUZFP_MAX_BITS 6144
+ * padding.  The bound keeps one wave's LDS stream image within a gfx950
+ * workgroup's LDS (160 KiB, hipDeviceAttributeMaxSharedMemoryPerBlock): the
+ * decoder's image at 16384 bits is 129 KiB plus 12 KiB of tables.  On a device
+ * with less LDS per workgroup a call whose image does not fit returns
+ * CUZFP_ERROR_INVALID_ARGUMENT. */
+#define CUZFP_MAX_BITS 16384
 
 /* Streams the host-memory pipeline is measured best with (callers' default
  * `nstreams` for cuzfp_hip_compress_host / decompress_host). */
@@ -108,13 +111,26 @@ int cuzfp_hip_decode(const uint64_t* d_stream, size_t stream_bytes, int type, un
 /* Host-memory end to end: the array and the stream live in
  * host memory; the library moves them through pinned staging buffers in
  * z-slab (3D) / y-slab (2D) / x-range (1D) chunks on `nstreams` HIP streams so
- * the copies overlap the kernels.  Synchronous; contiguous arrays only. */
+ * the copies overlap the kernels.  Synchronous; contiguous arrays only.
+ *
+ * Retention: the first call on a device allocates, and keeps for later calls,
+ * device buffers for the array and the stream (grown to the largest call, up
+ * to 1 GiB each; larger calls use buffers freed on return), `nstreams` HIP
+ * streams with their events, and (for pageable user buffers) pinned staging
+ * buffers of one chunk each (at most 64 MiB apiece).  This memory is outside
+ * any framework allocator (e.g. torch's caching allocator).  Calls on one
+ * device are serialised; calls on different devices run concurrently. */
 int cuzfp_hip_compress_host(const void* h_data, int type, unsigned nx, unsigned ny,
                             unsigned nz, unsigned maxbits, void* h_stream,
                             size_t stream_capacity, size_t* out_bytes, int nstreams);
 int cuzfp_hip_decompress_host(const void* h_stream, size_t stream_bytes, int type,
                               unsigned nx, unsigned ny, unsigned nz, unsigned maxbits,
                               void* h_data, int nstreams);
+
+/* Frees the host pipeline's retained buffers, streams and events for `device`
+ * (-1: the current device) after its pending work; the next host-pipeline call
+ * allocates them again.  Not a reference entry point. */
+int cuzfp_hip_release_host_cache(int device);
 
 /* Diagnostic, not a reference entry point: device-to-device copy of `bytes`
  * (a multiple of 16, both pointers 16-byte aligned) with 16-byte non-temporal

@@ -18,6 +18,19 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running (large arrays)")
 
 
+# The full-size parity tests of BASELINE's configurations against the
+# reference's hashes run first, so that a GPU run cut short (pytest -x, a
+# time limit) has still pinned every BASELINE config before the fuzz loops.
+_FIRST = ("test_golden_baseline_configs", "test_golden_1024_full_array", "test_golden_1024_slab")
+
+
+def pytest_collection_modifyitems(session, config, items):
+    def rank(item):
+        name = item.originalname or item.name
+        return _FIRST.index(name) if name in _FIRST else len(_FIRST)
+    items.sort(key=rank)  # stable: everything else keeps its order
+
+
 @pytest.fixture(scope="session")
 def restatement():
     import oracle

@@ -44,6 +44,14 @@ def test_header_symbols_exported(libs):
     assert not missing, missing
 
 
+def test_release_host_cache_bad_device(libs):
+    """cuzfp_hip_release_host_cache rejects device ordinals outside its cache
+    before touching the runtime (no GPU needed)."""
+    lib = cz.library()
+    assert lib.cuzfp_hip_release_host_cache(99) == 1
+    assert lib.cuzfp_hip_release_host_cache(-2) == 1
+
+
 def test_cpp_dropin_symbols(libs):
     out = subprocess.run(["nm", "-DC", "--defined-only", libs["cpp"]], capture_output=True, text=True).stdout
     assert "cuZFP::compress(cuZFP::zfp_stream*, cuZFP::zfp_field*)" in out
@@ -107,12 +115,12 @@ def test_argument_errors(libs):
 
 
 def test_maxbits_cap(libs):
-    """maxbits up to CUZFP_MAX_BITS (6144, above zfp's ZFP_MAX_BITS = 4171) is
-    accepted; above it every entry point rejects the call (the decoder's LDS
-    stream image would no longer fit a workgroup)."""
+    """maxbits up to CUZFP_MAX_BITS (16384, far above zfp's ZFP_MAX_BITS = 4171)
+    is accepted; above it every entry point rejects the call (the decoder's LDS
+    stream image would no longer fit a gfx950 workgroup's 160 KiB)."""
     lib = cz.library()
     cap = int(re.search(r"#define CUZFP_MAX_BITS (\d+)", open(HEADER).read()).group(1))
-    assert cap == 6144
+    assert cap == 16384
     assert cz.stream_bytes((16, 16, 16), np.float64, cap) == 64 * cap // 8
     with pytest.raises(cz.CodecError):
         cz.stream_bytes((16, 16, 16), np.float64, cap + 1)

@@ -1,0 +1,46 @@
+"""bench.py's multi-rank launcher on CPU: `python bench.py --gpus 2` with no
+torchrun around it starts its two ranks itself (torch.distributed.run, gloo in
+the dry-run mode, the CPU oracle standing in for the codec) and the line it
+prints reports both ranks -- the scaling run cannot under-report its ranks."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env_extra=None):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True,
+                          text=True, timeout=300, env=env, cwd=ROOT)
+
+
+def test_gpus2_launches_two_ranks():
+    r = _run(["--gpus", "2", "--dry-run-cpu", "--steps", "2", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 prints one line
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2
+    assert d["world_size_seen"] == 2
+    assert d["backend"] == "gloo"
+    assert len(d["rank_devices"]) == 2
+    assert d["value"] > 0
+
+
+def test_world_size_mismatch_is_an_error():
+    # a launcher that started fewer ranks than --gpus asks for: refused, no line
+    r = _run(["--gpus", "2", "--dry-run-cpu", "--steps", "1", "--warmup", "0"],
+             {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert "WORLD_SIZE" in r.stderr
+
+
+def test_single_rank_dry_run():
+    r = _run(["--dry-run-cpu", "--steps", "1", "--warmup", "0"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert d["n_gpus"] == 1 and d["world_size_seen"] == 1

@@ -107,14 +107,14 @@ def test_cli_long_header_and_stats(tools, tmp_path):
 
 @pytest.mark.gpu
 def test_cli_decode_failure_exits_nonzero(tools, tmp_path):
-    """A header whose maxbits the codec rejects (rate 100 in 3D f64: 6,400 bits
-    per block, past CUZFP_MAX_BITS) makes the CLI exit non-zero instead of
+    """A header whose maxbits the codec rejects (rate 300 in 3D f64: 19,200 bits
+    per block, past CUZFP_MAX_BITS = 16,384) makes the CLI exit non-zero instead of
     writing a zero-filled output."""
     import fuzz_cli
     cli, _ = tools
     raw = _gen(tools, tmp_path, "f64", [8, 8, 8])
     z = tmp_path / "big.z"
-    subprocess.check_call([fuzz_cli.CPU_ZFP, "-q", "-h", "-d", "-3", "8", "8", "8", "-r", "100", "-i", str(raw), "-z", str(z)])
+    subprocess.check_call([fuzz_cli.CPU_ZFP, "-q", "-h", "-d", "-3", "8", "8", "8", "-r", "300", "-i", str(raw), "-z", str(z)])
     out = tmp_path / "out.raw"
     r = subprocess.run([cli, "-q", "-h", "-z", str(z), "-o", str(out)], capture_output=True, text=True)
     assert r.returncode != 0

@@ -146,6 +146,32 @@ def test_emulation_random_streams(emu, restatement, dims, dtype):
 
 
 @pytest.mark.parametrize("dims", [1, 2, 3])
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_emulation_large_maxbits(emu, restatement, dims, dtype):
+    """Budgets past 2^13 (up to CUZFP_MAX_BITS = 16384, which the LDS of a
+    gfx950 workgroup allows): dense random streams make the plane decoder's
+    running bit counts pass the chunk entries' "not ended" marker (2^13), and
+    fields at those maxbits run every plane with budget to spare."""
+    from cuzfp_amd.datagen import splitmix_uniform
+    rng = np.random.default_rng(31 + dims)
+    shape = {1: (40,), 2: (12, 8), 3: (8, 4, 8)}[dims]
+    nb = int(np.prod([(s + 3) // 4 for s in shape]))
+    for mb in (8191, 8193, 9999, 16383, 16384):
+        for density in (0.5, 0.9, 0.97):
+            words = (nb * mb + 63) // 64
+            bits = rng.random(words * 64) < density
+            s = np.packbits(bits.reshape(-1, 8)[:, ::-1], axis=1).reshape(-1).view(np.uint64).copy()
+            want = restatement.decompress(s, shape, dtype, mb)
+            got = emu_decompress(emu, s, shape, dtype, mb)
+            assert np.array_equal(got.view(np.uint8), want.view(np.uint8)), (mb, density)
+        a = splitmix_uniform(shape, dtype, seed=mb)
+        s = restatement.compress(a, mb)
+        assert np.array_equal(emu_compress(emu, a, mb), s), mb
+        got = emu_decompress(emu, s, shape, dtype, mb)
+        assert np.array_equal(got.view(np.uint8), restatement.decompress(s, shape, dtype, mb).view(np.uint8)), mb
+
+
+@pytest.mark.parametrize("dims", [1, 2, 3])
 def test_emulation_budget_cuts(emu, restatement, dims):
     """Encoder output at every rate 1..32 (so the budget ends at every offset
     of the table decoder's window), smooth, noisy and rough fields: the table

@@ -402,14 +402,68 @@ def test_broadcast_view_encodes_materialised(cuda, restatement):
         cz.decode(w, (12, 16), torch.float32, mb, out=torch.empty(16, dtype=torch.float32, device=cuda).expand(12, 16))
 
 
+def test_host_cache_release(cuda, restatement):
+    """The host pipeline's retained buffers are freed by release_host_cache and
+    rebuilt by the next call; results are unchanged, pageable staging included."""
+    from cuzfp_amd.datagen import splitmix_uniform
+    a = splitmix_uniform((40, 36, 28), np.float32, seed=9)
+    mb = cz.rate_to_maxbits(8, np.float32, 3)
+    ref = restatement.compress(a, mb)
+    for _ in range(2):
+        s = cz.compress_host(a, mb)
+        assert np.array_equal(s, ref)
+        assert np.array_equal(cz.decompress_host(s, a.shape, np.float32, mb),
+                              restatement.decompress(ref, a.shape, np.float32, mb))
+        cz.release_host_cache()
+    cz.release_host_cache(0)  # twice in a row: a no-op
+
+
+def test_broadcast_view_side_stream(cuda, restatement):
+    """A broadcast view encoded on a side stream: the materialising copy runs on
+    that stream after the current stream's pending work (here the kernel that
+    writes the base tensor) and stays allocated until the encode has read it."""
+    import torch
+    side = torch.cuda.Stream(device=cuda)
+    mb = cz.rate_to_maxbits(8, np.float32, 3)
+    for trial in range(4):
+        base = torch.empty(64, dtype=torch.float32, device=cuda)
+        # exact values (power-of-two scale), written by a kernel queued on the current stream
+        base.copy_(torch.arange(64, dtype=torch.float32, device=cuda) * (trial + 1) / 64 - 0.5)
+        x = base.expand(40, 32, 64)
+        w = cz.encode(x, mb, stream=side)
+        del x, base
+        junk = torch.full((40 * 32 * 64,), float("nan"), device=cuda)  # would reuse a freed copy's memory
+        side.synchronize()
+        vals = np.arange(64, dtype=np.float32) * np.float32(trial + 1) / np.float32(64) - np.float32(0.5)
+        ref = restatement.compress(np.broadcast_to(vals, (40, 32, 64)).copy(), mb)
+        assert np.array_equal(w.cpu().numpy().view(np.uint64), ref), trial
+        del junk
+
+
+def test_copy_checks(cuda):
+    """cz.copy() refuses non-contiguous and host tensors."""
+    import torch
+    a = torch.zeros(64, 2, dtype=torch.float32, device=cuda)
+    with pytest.raises(ValueError):
+        cz.copy(a.t(), torch.empty(128, device=cuda))
+    with pytest.raises(ValueError):
+        cz.copy(torch.zeros(16), torch.empty(16, device=cuda))
+    b = torch.arange(1 << 12, dtype=torch.float32, device=cuda)
+    c = torch.empty_like(b)
+    cz.copy(b, c)
+    torch.cuda.synchronize()
+    assert torch.equal(b, c)
+
+
 @pytest.mark.parametrize("dims,dtype", [(3, np.float64), (3, np.float32), (2, np.float64), (1, np.float32)])
 def test_largest_maxbits(cuda, restatement, dims, dtype):
-    """maxbits at the cap (CUZFP_MAX_BITS = 6144): the widest LDS stream images
-    (one wave per workgroup) against the oracle."""
+    """maxbits at the cap (CUZFP_MAX_BITS = 16384, sized for gfx950's 160 KiB of
+    LDS a workgroup): the widest LDS stream images (one wave per workgroup,
+    dynamic LDS past 64 KiB) against the oracle, and the old 64 KiB cap."""
     from cuzfp_amd.datagen import splitmix_uniform
     shape = {1: (1000,), 2: (36, 28), 3: (12, 8, 20)}[dims]
     a = splitmix_uniform(shape, dtype, seed=3)
-    for mb in (6144, 6143, 4171):
+    for mb in (16384, 16383, 9999, 6144, 4171):
         words, y = _gpu_roundtrip(a, mb, cuda)
         ref = restatement.compress(a, mb)
         assert np.array_equal(words, ref), mb

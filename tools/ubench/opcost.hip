@@ -19,6 +19,7 @@
 #define ITERS 64
 
 #define R4(x) x x x x
+#define P4(op) op("%0") op("%1") op("%2") op("%3")
 #define CH8(op) op("%0") op("%1") op("%2") op("%3") op("%4") op("%5") op("%6") op("%7")
 
 // one instruction on chain register r, reading the other inputs from the
@@ -152,6 +153,56 @@ __device__ __forceinline__ void body32(uint32_t (&c)[8], uint32_t v, uint32_t s)
     asm volatile(CH8(LQ) "s_waitcnt lgkmcnt(0)\n" CH8(LA) : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]) : "v"(v), "s"(s) : "vcc", "memory");
 #undef LQ
 #undef LA
+  } else if constexpr (KIND == 60) {  // v_cmp (VCC) then v_cndmask_b32 (VOP2, VCC) on each chain: 2 instructions
+#define CV(r) "v_cmp_gt_u32 vcc, " r ", %8\nv_cndmask_b32 " r ", " r ", %8, vcc\n"
+    asm volatile(CH8(CV) : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]) : "v"(v), "s"(s) : "vcc");
+#undef CV
+  } else if constexpr (KIND == 61) {  // the same with the VOP3 compare into an SGPR pair and v_cndmask_b32_e64
+#define CS(r) "v_cmp_gt_u32_e64 s[20:21], " r ", %8\nv_cndmask_b32_e64 " r ", " r ", %8, s[20:21]\n"
+    asm volatile(CH8(CS) : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]) : "v"(v), "s"(s) : "vcc", "s20", "s21");
+#undef CS
+  } else if constexpr (KIND == 62) {  // v_cndmask_b32 (VOP2) with VCC written once by a v_cmp before the block
+    asm volatile("v_cmp_gt_u32 vcc, %0, %8\ns_nop 4\n" R4(CH8(OP_CNDMASK)) : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]) : "v"(v), "s"(s) : "vcc");
+  } else if constexpr (KIND == 63) {  // one dependent chain of v_add_u32 (latency)
+#define DA(r) "v_add_u32 %0, %0, %8\n"
+    asm volatile(R4(CH8(DA)) : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]) : "v"(v), "s"(s) : "vcc");
+#undef DA
+  } else if constexpr (KIND == 64) {  // one dependent chain of v_bfi_b32
+#define DB(r) "v_bfi_b32 %0, %9, %0, %8\n"
+    asm volatile(R4(CH8(DB)) : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]) : "v"(v), "s"(s) : "vcc");
+#undef DB
+  } else if constexpr (KIND == 65) {  // two dependent chains of v_add_u32, interleaved
+#define D2(r) "v_add_u32 %0, %0, %8\nv_add_u32 %1, %1, %8\n"
+    asm volatile(R4(P4(D2)) : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]) : "v"(v), "s"(s) : "vcc");
+#undef D2
+  } else if constexpr (KIND == 66) {  // SDWA move into the high half, low half preserved
+#define SD(r) "v_mov_b32_sdwa " r ", %8 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0\n"
+    asm volatile(R4(CH8(SD)) : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]) : "v"(v), "s"(s) : "vcc");
+#undef SD
+  } else if constexpr (KIND == 67) {  // packed 16-bit add
+#define PA(r) "v_pk_add_u16 " r ", " r ", %8\n"
+    asm volatile(R4(CH8(PA)) : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]) : "v"(v), "s"(s) : "vcc");
+#undef PA
+  } else if constexpr (KIND == 68) {  // v_lshlrev_b32 by an inline constant
+#define LC(r) "v_lshlrev_b32 " r ", 3, " r "\n"
+    asm volatile(R4(CH8(LC)) : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]) : "v"(v), "s"(s) : "vcc");
+#undef LC
+  } else if constexpr (KIND == 69) {  // v_cndmask_b32_e64 with an inline-constant source
+#define CK(r) "v_cndmask_b32_e64 " r ", 0, " r ", s[20:21]\n"
+    asm volatile("s_mov_b64 s[20:21], -1\n" R4(CH8(CK)) : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]) : "v"(v), "s"(s) : "vcc", "s20", "s21");
+#undef CK
+  } else if constexpr (KIND == 70) {  // v_and_or_b32 (VOP3, SGPR mask)
+#define AO(r) "v_and_or_b32 " r ", " r ", %9, %8\n"
+    asm volatile(R4(CH8(AO)) : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]) : "v"(v), "s"(s) : "vcc");
+#undef AO
+  } else if constexpr (KIND == 71) {  // v_add_u32 with the literal and VGPR swapped to e64 with an SGPR
+#define AS(r) "v_add_u32 " r ", %9, " r "\n"
+    asm volatile(R4(CH8(AS)) : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]) : "v"(v), "s"(s) : "vcc");
+#undef AS
+  } else if constexpr (KIND == 72) {  // v_sub_u32 with a VGPR from another chain (two VGPR sources, both changing)
+#define SV(r) "v_sub_u32 " r ", " r ", %0\n"
+    asm volatile(R4(CH8(SV)) : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]) : "v"(v), "s"(s) : "vcc");
+#undef SV
   } else if constexpr (KIND == 56) {  // readfirstlane + s_lshl + 3 fast
 #define RF(r) "v_readfirstlane_b32 s20, " r "\ns_lshl_b32 s21, 1, s20\nv_add_u32 " r ", " r ", %8\nv_xor_b32 " r ", " r ", %8\nv_add_u32 " r ", " r ", %8\n"
     asm volatile(CH8(RF) : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]) : "v"(v), "s"(s) : "vcc", "s20", "s21", "scc");
@@ -162,7 +213,6 @@ __device__ __forceinline__ void body32(uint32_t (&c)[8], uint32_t v, uint32_t s)
 }
 
 // 64-bit kinds: 4 chains of register pairs
-#define P4(op) op("%0") op("%1") op("%2") op("%3")
 #define OP_SHL64(r) "v_lshlrev_b64 " r ", 1, " r "\n"
 #define OP_SHR64(r) "v_lshrrev_b64 " r ", %4, " r "\n"
 #define OP_LADD64(r) "v_lshl_add_u64 " r ", " r ", 1, %5\n"
@@ -230,7 +280,7 @@ static void run(const char* name, uint32_t* d, uint64_t* c, int cus, int per_bod
   (void)scale;
 }
 
-int main() {
+int main(int argc, char** argv) {
   int dev = 0, cus = 0;
   hipGetDevice(&dev);
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -238,6 +288,27 @@ int main() {
   uint64_t* c;
   hipMalloc(&d, (size_t)cus * 4 * 256 * 4);
   hipMalloc(&c, (size_t)cus * 4 * 4 * 8);
+  if (argc > 1 && argv[1][0] == 'n') {  // the round-3 kinds only
+    run<60>("cmp+cnd vcc", d, c, cus, 64);
+    run<61>("cmp+cnd e64", d, c, cus, 64);
+    run<62>("cnd vcc fixed", d, c, cus);
+    run<13>("v_cndmask_b32", d, c, cus);
+    run<26>("v_cndmask_e64 s", d, c, cus);
+    run<69>("cnd e64 const", d, c, cus);
+    run<63>("dep add x1", d, c, cus);
+    run<65>("dep add x2", d, c, cus);
+    run<0>("v_add_u32", d, c, cus);
+    run<64>("dep bfi x1", d, c, cus);
+    run<5>("v_bfi_b32", d, c, cus);
+    run<66>("mov sdwa w1", d, c, cus);
+    run<67>("v_pk_add_u16", d, c, cus);
+    run<68>("lshl const", d, c, cus);
+    run<33>("v_lshlrev_b32 v", d, c, cus);
+    run<70>("v_and_or_b32", d, c, cus);
+    run<71>("v_add_u32 sgpr", d, c, cus);
+    run<72>("v_sub vv", d, c, cus);
+    return 0;
+  }
   run<0>("v_add_u32", d, c, cus);
   run<1>("v_add_u32_e64", d, c, cus);
   run<2>("v_ashrrev_i32", d, c, cus);
