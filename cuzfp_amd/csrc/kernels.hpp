@@ -587,6 +587,7 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS, t
 #else
   if (b < g.nblocks) gather<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
 #endif
+  // (one copy a workgroup behind a barrier measured slower: 28.0 -> 28.4 us at 256^3)
 #pragma unroll
   for (uint32_t i = 0; i < kTabPieces / kLanes; i++) ((uint4*)stab)[lane + i * kLanes] = tab16[i];
 #if defined(CUZFP_EXP_PAD) && defined(__HIP_DEVICE_COMPILE__) && CUZFP_EXP_PAD_AT == 0

@@ -709,7 +709,8 @@ ZFP_HD PlaneLen plane_len(uint32_t nf, uint32_t bl, uint32_t L) {
 }
 
 template <int DIMS, typename PW, typename Writer>
-ZFP_HD void encode_plane_one_put(PW x, unsigned nf, uint32_t rl, const PlaneLen& pl, unsigned& n, Writer& wr) {
+ZFP_HD void encode_plane_one_put(PW x, unsigned nf, uint64_t r, const PlaneLen& pl, unsigned& n, Writer& wr) {
+  const uint32_t rl = (uint32_t)r;
   constexpr unsigned N = 1u << (2 * DIMS);
   const uint32_t width = pl.width;
   // "1" + r with every one doubled: one table entry a byte of r (3D: r < 2^15,
@@ -718,7 +719,9 @@ ZFP_HD void encode_plane_one_put(PW x, unsigned nf, uint32_t rl, const PlaneLen&
   uint32_t G = e0 >> 5;
   if constexpr (N > 4) G |= wr.sp1(byte_off4<1>(rl)) << (e0 & 31u);
   const uint32_t g = low_bits(G, width);
-  const uint64_t code = (uint64_t)x ^ ((uint64_t)(rl ^ g) << nf);
+  // r < 2^32 here, so r ^ g is (r's high word, rl ^ g): the shift takes r's
+  // register pair as it is instead of a zero-extended copy of rl ^ g
+  const uint64_t code = (uint64_t)x ^ ((r ^ (uint64_t)g) << nf);
   wr.put(code, pl.len);
   n = pl.nn - pl.imp;  // min(nn, N-1)
 }
@@ -787,14 +790,14 @@ ZFP_HD void encode_plane_step(PW x, unsigned& n, Writer& wr) {
   const PlaneLen pl = plane_len<DIMS>(nf, bl, L);
   if constexpr (N <= 16) {
     // r has at most 16 bits and the code at most 48: always one put
-    encode_plane_one_put<DIMS>(x, nf, rl, pl, n, wr);
+    encode_plane_one_put<DIMS>(x, nf, r, pl, n, wr);
   } else {
     // one put while every lane's code fits 64 bits with r < 2^15 (3D rate 8
     // on smooth data: ~26 of ~29 plane steps, tools/coder_stats.cpp);
     // otherwise the wide step for the whole wave
     const bool ok = (r >> 15) == 0 && pl.len <= 64u;
     if (__builtin_expect(!any_lane(!ok), 1))
-      encode_plane_one_put<DIMS>(x, nf, rl, pl, n, wr);
+      encode_plane_one_put<DIMS>(x, nf, r, pl, n, wr);
     else
       encode_plane_wide((uint64_t)x, n, wr);
   }
@@ -1366,7 +1369,9 @@ ZFP_HD PW decode_plane_fast(unsigned& bits, unsigned& n, Reader& rd, bool& slow,
   } else {
     uint32_t e2a, e2b;
     rd.chunks_fast(g, e1, e2a, e2b);
-    e2 = keep_if_bit13((e1 & kEntryState) ? e2b : e2a, e1);
+    // the exit state (bit 31) as a mask by one arithmetic shift, the select
+    // by v_bfi (a compare and a v_cndmask otherwise: two slow-issue VALU ops)
+    e2 = keep_if_bit13(bfi_v((uint32_t)((int32_t)e1 >> 31), e2b, e2a), e1);
   }
   const uint32_t S = e1 + e2;
   const uint32_t npos = S >> kPosShift & 31u;
