@@ -77,6 +77,9 @@ def parse():
     p.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     p.add_argument("--per-graph", type=int, default=0,
                    help="steps captured per hipGraph (default: the largest divisor of --steps up to 200)")
+    p.add_argument("--kernel-ms", type=float, default=50.0,
+                   help="GPU time each per-kernel measurement (encode_ms, decode_ms) runs for, back to back just "
+                        "before the warmup steps")
     p.add_argument("--no-config5", action="store_true", help="skip BASELINE configs[4] (1024^3 sharded)")
     p.add_argument("--config5-edge", type=int, default=1024, help="edge of configs[4]'s global array")
     p.add_argument("--config5-steps", type=int, default=10)
@@ -231,14 +234,14 @@ def cpu_baseline(a: np.ndarray, maxbits: int):
 
 
 def run_config5(E: int, steps: int, world: int, rank: int, dev, graphed, dist):
-    """BASELINE configs[4] at this N: one E^3 f32 polynomial array at
-    rate 8 strong-scaled over the N ranks as z-slabs of E/N planes.  Each rank
-    encodes and decodes its slab (no communication); the step time is the max
-    over ranks of K steps between barriers.  Then, outside the timed region,
-    the RCCL all-gather that assembles the global stream on every rank, timed
-    with HIP events on the launch stream; and parity: every rank's segment and
-    the gathered stream against the reference's SHA-256s, the round-trip error
-    against the reference's."""
+    """BASELINE configs[4] at this N, GPU phase: one E^3 f32 polynomial
+    array at rate 8 strong-scaled over the N ranks as z-slabs of E/N planes.  Each
+    rank encodes and decodes its slab (no communication); the step time is the
+    max over ranks of K steps between barriers.  Then, outside that timed region,
+    the RCCL all-gather that assembles the global stream on every rank, timed with
+    HIP events on the launch stream.  Returns the record and what finish_config5
+    needs for the parity check (host-side hashing, done after the headline's timed
+    region so that the GPU does not idle for seconds just before it)."""
     import torch
     import cuzfp_amd as cz
     from cuzfp_amd import dist as zd
@@ -255,8 +258,7 @@ def run_config5(E: int, steps: int, world: int, rank: int, dev, graphed, dist):
         cz.decode(words, sh.shape, x.dtype, maxbits, out=y)
 
     step()
-    torch.cuda.synchronize()
-    max_err = float((y - x).abs().max().item())
+    err = (y - x).abs().max()  # stays on the device until finish_config5
 
     def allmax(v: float) -> float:
         t = torch.tensor([v], dtype=torch.float64, device=dev)
@@ -304,17 +306,7 @@ def run_config5(E: int, steps: int, world: int, rank: int, dev, graphed, dist):
     cz.encode(x, maxbits, out=words)
     torch.cuda.synchronize()
 
-    gold = None
-    gpath = os.path.join(ROOT, "tests", "golden", "golden.json")
-    if os.path.exists(gpath):
-        gold = json.load(open(gpath))["cases"].get(f"baseline/3d_f32_{E}_r8/polynomial")
-    local = words.cpu().numpy()
-    slab_ok = None
-    if gold and world > 1 and f"slab_sha256_n{world}" in gold:
-        slab_ok = hashlib.sha256(local.tobytes()).hexdigest() == gold[f"slab_sha256_n{world}"][rank]
-        slab_ok = allmax(0.0 if slab_ok else 1.0) == 0.0
-
-    ag_s = None
+    ag_s, full = None, None
     if world > 1:
         full = zd.allgather_stream(words)
         torch.cuda.synchronize()
@@ -328,13 +320,39 @@ def run_config5(E: int, steps: int, world: int, rank: int, dev, graphed, dist):
         torch.cuda.synchronize()
         dist.barrier()
         ag_s = allmax(e0.elapsed_time(e1) / 5 * 1e-3)
-        full_host = full.cpu().numpy() if rank == 0 else None
-        del full
-    else:
-        full_host = local
+        if rank != 0:
+            full = None
     out = zd.sharded_summary(sh, 4, step_s, enc_s, dec_s, HBM_PEAK_GBS, ag_s)
     out["steps"] = steps
-    out["max_abs_err"] = allmax(max_err)
+    del x, y
+    return {"record": out, "E": E, "words": words, "full": full, "err": err}
+
+
+def finish_config5(st: dict, world: int, rank: int, dev, dist) -> dict:
+    """configs[4]'s parity, on the host: every rank's segment against the
+    reference's SHA-256 of its word range, the gathered stream (rank 0) against
+    the reference's whole-stream hash, the round-trip error against the
+    reference's (tests/golden/golden.json)."""
+    import torch
+    out, E = st["record"], st["E"]
+
+    def allmax(v: float) -> float:
+        t = torch.tensor([v], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    gold = None
+    gpath = os.path.join(ROOT, "tests", "golden", "golden.json")
+    if os.path.exists(gpath):
+        gold = json.load(open(gpath))["cases"].get(f"baseline/3d_f32_{E}_r8/polynomial")
+    local = st["words"].cpu().numpy()
+    slab_ok = None
+    if gold and world > 1 and f"slab_sha256_n{world}" in gold:
+        slab_ok = hashlib.sha256(local.tobytes()).hexdigest() == gold[f"slab_sha256_n{world}"][rank]
+        slab_ok = allmax(0.0 if slab_ok else 1.0) == 0.0
+    full_host = (st["full"].cpu().numpy() if st["full"] is not None else None) if world > 1 else local
+    out["max_abs_err"] = allmax(float(st["err"].item()))
     if rank == 0:
         got = hashlib.sha256(full_host.tobytes()).hexdigest()
         out["parity"] = {"reference_sha256": gold["stream_sha256"] if gold else None,
@@ -342,7 +360,7 @@ def run_config5(E: int, steps: int, world: int, rank: int, dev, graphed, dist):
                          "stream_matches_reference": (got == gold["stream_sha256"]) if gold else None,
                          "slabs_match_reference_word_ranges": slab_ok,
                          "max_abs_err_matches_reference": (out["max_abs_err"] == gold["max_abs_err"]) if gold else None}
-    del x, y, words
+    st.clear()
     torch.cuda.empty_cache()
     return out
 
@@ -422,40 +440,55 @@ def main():
     step()
     torch.cuda.synchronize()
     max_err = float((y.double() - x.double()).abs().max().item())
-    parity = None
-    gpath = os.path.join(ROOT, "tests", "golden", "golden.json")
-    key = {("float32", 8.0): "baseline/3d_f32_256_r8", ("float64", 16.0): "baseline/3d_f64_256_r16"}.get(
-        (args.dtype, args.rate))
-    if key and dims == 3 and n == 256 and world == 1 and not strong and os.path.exists(gpath):
-        rec = json.load(open(gpath))["cases"].get(f"{key}/{args.field}")
-        if rec:
-            got = hashlib.sha256(words.cpu().numpy().tobytes()).hexdigest()
-            parity = "stream sha256 == reference zfp 0.5.0" if got == rec["stream_sha256"] else "MISMATCH"
+    # Order of the GPU work.  The other GPU measurements of the line (BASELINE
+    # configs[4], the copy calibrator, the RCCL all-gather, per-kernel times) run
+    # before the timed region, with every graph captured up front and every
+    # host-side check (stream hashes, the CPU baseline) after it, so that the
+    # timed steps start on a GPU that has been busy up to that point: after the
+    # GPU idles (a host-side hash of the 1 GiB configs[4] stream takes seconds)
+    # its clocks ramp again over the first ~10 ms of work, and a 20-step run
+    # measured 8-11 % below the same steps on a busy GPU (1,150-1,203 vs
+    # 1,294 GB/s on one box).  The timed region itself is unchanged: W warmup
+    # steps, then exactly K steps.
+    per_graph = args.per_graph or next(c for c in range(min(200, args.steps), 0, -1) if args.steps % c == 0)
+    if args.steps % per_graph:
+        raise SystemExit(f"--per-graph {per_graph} does not divide --steps {args.steps}")
+    run = graphed(step, per_graph)
+    run()  # the graph's first replay uploads it: never inside the timed region
+    enc_graph = graphed(lambda: cz.encode(x, maxbits, out=words), 50)
+    dec_graph = graphed(lambda: cz.decode(words, shape, x.dtype, maxbits, out=y), 50)
+    enc_graph()
+    dec_graph()
 
-    # The other GPU measurements of the line (per-kernel times, the copy
-    # calibrator, the RCCL all-gather, BASELINE configs[4]) run before the timed
-    # region rather than after it, so that the timed steps run on a GPU that has
-    # been busy for a while: from a cold start the clocks ramp over the first
-    # ~10 ms of work, and a 20-step run timed first measured 8-11 % below the
-    # same steps timed after them (1,150 vs 1,294 GB/s on one box).  The timed
-    # region itself is unchanged: W warmup steps, then exactly K steps.
-    # per-kernel durations with HIP events on the launch stream
-    def time_kernel(fn, reps):  # reps launches as hipGraphs of 50
-        r = graphed(fn, 50)
-        r()
+    c5 = None
+    if not args.no_config5 and dims == 3 and args.dtype == "float32" and not strong:
+        try:
+            c5 = run_config5(args.config5_edge, args.config5_steps, world, rank, dev, graphed, dist)
+        except torch.cuda.OutOfMemoryError as e:  # pragma: no cover
+            c5 = {"error": f"out of memory: {e}"}
+
+    # per-kernel durations with HIP events on the launch stream: replays of a
+    # hipGraph of 50 launches, back to back for at least `min_ms` of GPU time
+    # (sized from one replay), so each mean is over thousands of launches on a
+    # GPU under sustained load -- the state the timed steps then start in
+    def time_kernel(r, min_ms, then=None):
         torch.cuda.synchronize()
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record(stream)
-        for _ in range(reps // 50):
-            r()
+        r()
         e1.record(stream)
         torch.cuda.synchronize()
-        return e0.elapsed_time(e1) / (reps // 50 * 50)
+        n = max(2, int(min_ms / max(e0.elapsed_time(e1), 1e-3)) + 1)
+        e0.record(stream)
+        for _ in range(n):
+            r()
+        e1.record(stream)
+        if then is not None:
+            then()  # queued behind the measured launches, before the synchronize
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / (n * 50), n * 50
 
-    reps = 50 * max(2, args.steps // 50)
-    enc_ms = time_kernel(lambda: cz.encode(x, maxbits, out=words), reps)
-    dec_ms = time_kernel(lambda: cz.decode(words, shape, x.dtype, maxbits, out=y), reps)
 
     # achievable HBM bandwidth on this box: the library's 16-byte
     # non-temporal copy kernel (cuzfp_hip_copy, the codec's access width and
@@ -506,25 +539,27 @@ def main():
                      "backend": "nccl (RCCL)"}
         del full
 
-    config5 = None
-    if not args.no_config5 and dims == 3 and args.dtype == "float32" and not strong:
-        try:
-            config5 = run_config5(args.config5_edge, args.config5_steps, world, rank, dev, graphed, dist)
-        except torch.cuda.OutOfMemoryError as e:  # pragma: no cover
-            config5 = {"error": f"out of memory: {e}"}
+    # (last before the warmup steps: the ~100 ms of back-to-back kernels bring
+    # the GPU to the clocks it holds under load, see "Order of the GPU work")
+    # The W warmup steps are queued right behind the decode timing's last launch
+    # (as replays of the timed graph and of a graph of the W % per_graph rest),
+    # so the GPU does not idle between the two.
+    warm_rest = graphed(step, args.warmup % per_graph) if args.warmup % per_graph else None
+    if warm_rest is not None:
+        warm_rest()  # upload
 
-    per_graph = args.per_graph or next(c for c in range(min(200, args.steps), 0, -1) if args.steps % c == 0)
-    if args.steps % per_graph:
-        raise SystemExit(f"--per-graph {per_graph} does not divide --steps {args.steps}")
-    run = graphed(step, per_graph)
-    # W warmup steps, replayed as the timed steps are (the last W % per_graph eagerly)
-    for _ in range(args.warmup // per_graph):
-        run()
-    for _ in range(args.warmup % per_graph):
-        step()
-    if args.warmup < per_graph:
-        run()  # the graph's first replay uploads it: never inside the timed region
-    torch.cuda.synchronize()
+    def warmup():
+        for _ in range(args.warmup // per_graph):
+            run()
+        if warm_rest is not None:
+            warm_rest()
+
+    t_pre = time.perf_counter()
+    enc_ms, enc_n = time_kernel(enc_graph, args.kernel_ms)
+    dec_ms, dec_n = time_kernel(dec_graph, args.kernel_ms, then=warmup)
+    pre_timed = {"what": "per-kernel timing (encode_ms, decode_ms): back-to-back hipGraph replays, then the W "
+                         "warmup steps", "encode_launches": enc_n, "decode_launches": dec_n,
+                 "wall_ms": round((time.perf_counter() - t_pre) * 1e3, 1)}
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -544,6 +579,21 @@ def main():
         dist.all_reduce(t_local, op=dist.ReduceOp.MAX)
     elapsed = float(t_local.item())
     gpu_ms_per_step = ev0.elapsed_time(ev1) / args.steps
+
+    # host-side checks, after the timed region: the stream's SHA-256 against the
+    # reference's (N=1; the timed steps rewrote the same words), configs[4]'s parity
+    parity = None
+    gpath = os.path.join(ROOT, "tests", "golden", "golden.json")
+    key = {("float32", 8.0): "baseline/3d_f32_256_r8", ("float64", 16.0): "baseline/3d_f64_256_r16"}.get(
+        (args.dtype, args.rate))
+    if key and dims == 3 and n == 256 and world == 1 and not strong and os.path.exists(gpath):
+        rec = json.load(open(gpath))["cases"].get(f"{key}/{args.field}")
+        if rec:
+            got = hashlib.sha256(words.cpu().numpy().tobytes()).hexdigest()
+            parity = "stream sha256 == reference zfp 0.5.0" if got == rec["stream_sha256"] else "MISMATCH"
+    config5 = None
+    if c5 is not None:
+        config5 = c5 if "error" in c5 else finish_config5(c5, world, rank, dev, dist)
 
     n_in = a.nbytes
     value = n_in * world * args.steps / elapsed / 1e9
@@ -651,6 +701,7 @@ def main():
             "config5": config5,
             "max_abs_err": max_err,
             "parity": parity,
+            "pre_timed_gpu_work": pre_timed,
             **ranks,
         }
         print(json.dumps(result), flush=True)

@@ -222,7 +222,11 @@ struct LdsReader {
   // so the offsets are built with the fewest instructions, three-input ones
   // included.)
   __device__ __forceinline__ uint32_t tab(uint32_t byte_off) const {
+#if defined(CUZFP_EXP_GTAB)  // timing experiment: the tables read through the vector L1 instead of LDS
+    return *(const uint32_t*)((const char*)g_chunk_lut.e + byte_off);
+#else
     return *(lds_u32*)((uintptr_t)(lds_u32*)lut32 + byte_off);
+#endif
   }
   // g with every bit cleared unless its leading group test (bit 0) is 1: a
   // lane whose test reads "0" (no new ones: about half the lane-steps) looks
@@ -545,8 +549,14 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS, t
   // for it, not for the block's gathers
   constexpr uint32_t kTabPieces = kSpreadTabBytes / 16;  // two 16-byte pieces a lane
   uint4 tab16[kTabPieces / kLanes];
+  // (1D reads entries 0-15 of table 0 alone: r = x >> n < 2^4, so lanes 0-3
+  // copy 64 bytes instead of the whole 2 KiB)
+  if constexpr (DIMS == 1) {
+    if (lane < 4) tab16[0] = ((const uint4*)g_spread_tab.e)[lane];
+  } else {
 #pragma unroll
-  for (uint32_t i = 0; i < kTabPieces / kLanes; i++) tab16[i] = ((const uint4*)g_spread_tab.e)[lane + i * kLanes];
+    for (uint32_t i = 0; i < kTabPieces / kLanes; i++) tab16[i] = ((const uint4*)g_spread_tab.e)[lane + i * kLanes];
+  }
   if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);  // lowered through the plane loop (progress_priority)
   lds_spread* lut = (lds_spread*)stab;
   ZFP_STAMP_HWID();
@@ -588,8 +598,12 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS, t
   if (b < g.nblocks) gather<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
 #endif
   // (one copy a workgroup behind a barrier measured slower: 28.0 -> 28.4 us at 256^3)
+  if constexpr (DIMS == 1) {
+    if (lane < 4) ((uint4*)stab)[lane] = tab16[0];
+  } else {
 #pragma unroll
-  for (uint32_t i = 0; i < kTabPieces / kLanes; i++) ((uint4*)stab)[lane + i * kLanes] = tab16[i];
+    for (uint32_t i = 0; i < kTabPieces / kLanes; i++) ((uint4*)stab)[lane + i * kLanes] = tab16[i];
+  }
 #if defined(CUZFP_EXP_PAD) && defined(__HIP_DEVICE_COMPILE__) && CUZFP_EXP_PAD_AT == 0
   exp_pad(lane);  // timing experiment: dummy VALU work while the gathers are in flight
 #endif
@@ -679,8 +693,10 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
       blk = ((uint64_t)__builtin_amdgcn_alignbit(a1, a0, s0) |
              ((uint64_t)__builtin_amdgcn_alignbit(a2, a1, s0) << 32)) & lowmask(g.maxbits);
     }
+#if !defined(CUZFP_EXP_GTAB)
     for (uint32_t i = kLutFrom + threadIdx.x; i < sizeof(ChunkLut) / 16; i += blockDim.x)
       ((uint4*)lut)[i] = ((const uint4*)g_chunk_lut.e)[i];
+#endif
   } else {
     const uint32_t D = (g.maxbits + 31) >> 5;  // dwords per block
     const bool vec = (g.maxbits & 127) == 0 && g.vec_io;
@@ -860,6 +876,8 @@ int launch_encode_t(const void* data, const Geometry& g, bool fast, uint64_t* st
   else if (fast && aligned)
     hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, true, true>), grid, block, lds, st, d, gg, stream);
 #if defined(CUZFP_EXP_ONLY3D)
+  else if (fast)
+    hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, true, false>), grid, block, lds, st, d, gg, stream);
   else
     return CUZFP_ERROR_UNSUPPORTED_TYPE;
 #else
@@ -929,7 +947,11 @@ template <typename Scalar>
 int launch_encode_type(const Problem& p, const void* data, bool fast, uint64_t* stream,
                        uint32_t wave0, uint32_t nwaves, hipStream_t st) {
 #if defined(CUZFP_EXP_ONLY3D)
-  if (p.dims == 3 && fast) return launch_encode_t<Scalar, 3>(data, p.g, fast, stream, wave0, nwaves, st);
+#ifndef CUZFP_EXP_DIMS
+#define CUZFP_EXP_DIMS 3
+#endif
+  if (p.dims == CUZFP_EXP_DIMS && fast)
+    return launch_encode_t<Scalar, CUZFP_EXP_DIMS>(data, p.g, fast, stream, wave0, nwaves, st);
 #endif
   (void)p, (void)data, (void)fast, (void)stream, (void)wave0, (void)nwaves, (void)st;
   return CUZFP_ERROR_UNSUPPORTED_TYPE;
@@ -938,7 +960,8 @@ template <typename Scalar>
 int launch_decode_type(const Problem& p, const uint64_t* stream, bool fast, void* data,
                        uint32_t wave0, uint32_t nwaves, hipStream_t st) {
 #if defined(CUZFP_EXP_ONLY3D)
-  if (p.dims == 3 && fast) return launch_decode_t<Scalar, 3>(stream, p.g, fast, data, wave0, nwaves, st);
+  if (p.dims == CUZFP_EXP_DIMS && fast)
+    return launch_decode_t<Scalar, CUZFP_EXP_DIMS>(stream, p.g, fast, data, wave0, nwaves, st);
 #endif
   (void)p, (void)data, (void)fast, (void)stream, (void)wave0, (void)nwaves, (void)st;
   return CUZFP_ERROR_UNSUPPORTED_TYPE;

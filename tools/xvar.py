@@ -2,7 +2,8 @@
 
   python tools/xvar.py build NAME "-DFLAG=1 ..." [NAME "FLAGS" ...]   # here
   python tools/xvar.py isa NAME [NAME ...]                            # here: ISA histograms
-  python tools/xvar.py run [--size S] [--field F] NAME [NAME ...]      # GPU box
+  python tools/xvar.py run [--size S] [--field F] [--dims D --rate R] NAME [NAME ...]   # GPU box
+    (variants built with -DCUZFP_EXP_DIMS=D for 1D / 2D)
 
 Unlike tools/variants.py (a full library per variant), a variant here compiles
 only the 3D fast-gather float kernels (-DCUZFP_EXP_ONLY3D); the other scalar
@@ -27,13 +28,16 @@ STUB = os.path.join(OUT, "_stub")
 LLVM = "/opt/rocm/lib/llvm/bin"
 
 
-def _stub_objs():
+def _stub_objs(unit):
+    """Stub objects for every scalar type but `unit`'s, plus the C-ABI."""
     from cuzfp_amd import build as b
     os.makedirs(STUB, exist_ok=True)
     hdrs = [os.path.join(b.CSRC, h) for h in b.HEADERS] + [os.path.join(b.INC, "cuzfp_hip.h")]
     objs, procs = [], []
-    for u, flags in (("inst_f64", ["-DCUZFP_EXP_STUB"]), ("inst_i32", ["-DCUZFP_EXP_STUB"]),
-                     ("inst_i64", ["-DCUZFP_EXP_STUB"]), ("capi", [])):
+    for u, flags in (("inst_f32", ["-DCUZFP_EXP_STUB"]), ("inst_f64", ["-DCUZFP_EXP_STUB"]),
+                     ("inst_i32", ["-DCUZFP_EXP_STUB"]), ("inst_i64", ["-DCUZFP_EXP_STUB"]), ("capi", [])):
+        if u == unit:
+            continue
         o = os.path.join(STUB, u + ".o")
         objs.append(o)
         src = os.path.join(b.CSRC, u + ".hip")
@@ -43,20 +47,26 @@ def _stub_objs():
     return objs
 
 
+def _unit(flags: str) -> str:  # "@f64" in a variant's flags: the double kernels
+    return "inst_f64" if "@f64" in flags.split() else "inst_f32"
+
+
 def build(pairs):
     from cuzfp_amd import build as b
-    stubs = _stub_objs()
     procs = []
     for name, flags in pairs:
         d = os.path.join(OUT, name)
         os.makedirs(d, exist_ok=True)
-        procs.append(subprocess.Popen([b.HIPCC, *b.CXXFLAGS, "-DCUZFP_EXP_ONLY3D", *flags.split(), "-c",
-                                       os.path.join(b.CSRC, "inst_f32.hip"), "-o", os.path.join(d, "inst_f32.o")]))
+        u = _unit(flags)
+        fl = [f for f in flags.split() if f != "@f64"]
+        procs.append(subprocess.Popen([b.HIPCC, *b.CXXFLAGS, "-DCUZFP_EXP_ONLY3D", *fl, "-c",
+                                       os.path.join(b.CSRC, u + ".hip"), "-o", os.path.join(d, "inst_f32.o")]))
     assert all(p.wait() == 0 for p in procs)
     for name, flags in pairs:
         d = os.path.join(OUT, name)
         subprocess.check_call([b.HIPCC, f"--offload-arch={b.ARCH}", "-shared", "-fPIC", "-o",
-                               os.path.join(d, "libcuzfp_hip.so"), os.path.join(d, "inst_f32.o"), *stubs])
+                               os.path.join(d, "libcuzfp_hip.so"), os.path.join(d, "inst_f32.o"),
+                               *_stub_objs(_unit(flags))])
         with open(os.path.join(d, "flags.txt"), "w") as f:
             f.write(flags + "\n")
     print("built", [n for n, _ in pairs])
@@ -105,14 +115,14 @@ os.environ['CUZFP_HIP_LIB'] = {lib!r}
 import numpy as np
 import cuzfp_amd as cz
 from cuzfp_amd.datagen import polynomial_field, splitmix_uniform
-shape = ({size},)*3
-arr = polynomial_field(shape, 'float32') if {field!r} == 'polynomial' else splitmix_uniform(shape, 'float32')
+shape = ({size},)*{dims}
+arr = polynomial_field(shape, {dtype!r}) if {field!r} == 'polynomial' else splitmix_uniform(shape, {dtype!r})
 x = torch.from_numpy(arr).cuda()
-mb = cz.rate_to_maxbits(8, arr.dtype, 3)
+mb = cz.rate_to_maxbits({rate}, arr.dtype, {dims})
 w = cz.encode(x, mb); y = cz.decode(w, shape, x.dtype, mb)
 torch.cuda.synchronize()
 gold = json.load(open(os.path.join({root!r}, 'tests', 'golden', 'golden.json')))['cases']
-key = 'baseline/3d_f32_%d_r8/%s' % ({size}, {field!r})
+key = 'baseline/%dd_%s_%s_r%d/%s' % ({dims}, 'f32' if {dtype!r} == 'float32' else 'f64', '1M' if {size} == 1 << 20 else str({size}), {rate}, {field!r})
 ok = None
 if key in gold:
     s = hashlib.sha256(w.cpu().numpy().tobytes()).hexdigest() == gold[key]['stream_sha256']
@@ -138,16 +148,16 @@ print(json.dumps(dict(enc_us=t(lambda: cz.encode(x, mb, out=w)), dec_us=t(lambda
 """
 
 
-def run(names, size, fields):
+def run(names, size, fields, dims=3, rate=8, dtype="float32"):
     for field in fields:
         for name in names:
             lib = os.path.join(OUT, name, "libcuzfp_hip.so")
-            code = CODE.format(root=ROOT, lib=lib, size=size, field=field)
+            code = CODE.format(root=ROOT, lib=lib, size=size, field=field, dims=dims, rate=rate, dtype=dtype)
             r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
             if r.returncode:
                 print(name, "FAILED", r.stderr[-800:], flush=True)
                 sys.exit(r.returncode)
-            print(f"{name:12s} {field:10s} {size} {r.stdout.strip()}", flush=True)
+            print(f"{name:12s} {field:10s} {dims}D {size} r{rate} {r.stdout.strip()}", flush=True)
 
 
 if __name__ == "__main__":
@@ -159,11 +169,17 @@ if __name__ == "__main__":
         isa(sys.argv[2:])
     elif cmd == "run":
         a = sys.argv[2:]
-        size, fields = 256, ["polynomial"]
+        size, fields, dims, rate, dtype = 256, ["polynomial"], 3, 8, "float32"
         while a and a[0].startswith("--"):
             if a[0] == "--size":
                 size = int(a[1])
             elif a[0] == "--field":
                 fields = a[1].split(",")
+            elif a[0] == "--dims":
+                dims = int(a[1])
+            elif a[0] == "--rate":
+                rate = int(a[1])
+            elif a[0] == "--dtype":
+                dtype = a[1]
             a = a[2:]
-        run(a, size, fields)
+        run(a, size, fields, dims, rate, dtype)
