@@ -82,8 +82,8 @@ def main():
     obj = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "build", "obj", "inst_f32.o")
     ks = kernels(disassemble(obj))
     for name, ops in ks.items():
-        enc = re.search(r"zfp_encodeIfLi3ELb1ELb1ELb(\d)", name)
-        dec = re.search(r"zfp_decodeIfLi3ELb1ELb(\d)ELb0", name)
+        enc = re.search(r"zfp_encodeI[fd]Li3ELb1ELb1ELb(\d)", name)
+        dec = re.search(r"zfp_decodeI[fd]Li3ELb1ELb(\d)ELb0", name)
         if not (enc or dec):
             continue
         kind = "encode" if enc else "decode"
