@@ -18,7 +18,9 @@ of the inverse transpose), transpose + inverse lifting + stores.  Counts are
 static (each instruction once): the plane loops are unrolled, so a phase's
 count is close to what one wave executes, except for the rare paths (the
 encoder's wide step, the decoder's lut_finish / general decoder), which are
-listed separately where they can be told apart.
+listed separately: the compiler lays them out after the main path's
+s_endpgm.  The dynamic per-wave counts are SQ_INSTS_VALU / SQ_WAVES in
+profiles/r03_counters.txt.
 """
 from __future__ import annotations
 
@@ -95,13 +97,20 @@ def main():
             t1 = first(ops, lambda o: o == "ds_read_b32", t0)
             print("   prologue (gathers, exponent, quantisation, lifting)\n          " + summary(ops[:t0]))
             print("   transpose\n          " + summary(ops[t0:t1]))
-            print("   plane coder (one-put steps, wide steps) and copy-out\n          " + summary(ops[t1:]))
+            e = first(ops, lambda o: o == "s_endpgm", t1)
+            print("   plane coder (one-put steps, wide steps) and copy-out\n          " + summary(ops[t1:e + 1]))
+            e = first(ops, lambda o: o == "s_endpgm", t1)
+            if e + 1 < len(ops):
+                print("   out-of-line blocks after s_endpgm\n          " + summary(ops[e + 1:]))
         else:
             p0 = first(ops, lambda o: o.startswith("ds_read2st64"))
             t0 = first(ops, lambda o: o == "v_perm_b32", p0)
+            e = first(ops, lambda o: o == "s_endpgm", t0)
             print("   prologue (copy-in, header)\n          " + summary(ops[:p0]))
-            print("   plane decoder (fast steps, lut_finish, general decoder)\n          " + summary(ops[p0:t0]))
-            print("   transpose, inverse lifting, dequantisation, stores\n          " + summary(ops[t0:]))
+            print("   plane decoder, fast steps (in line)\n          " + summary(ops[p0:t0]))
+            print("   transpose, inverse lifting, dequantisation, stores\n          " + summary(ops[t0:e + 1]))
+            print("   out-of-line rare paths after s_endpgm (lut_finish, general decoder)\n          "
+                  + summary(ops[e + 1:]))
 
 
 if __name__ == "__main__":
