@@ -187,6 +187,7 @@ struct LdsReader {
   const uint32_t* lds32;
   const uint32_t* lut32;  // the workgroup's copy of the chunk tables (static LDS)
   uint32_t pos;
+  uint32_t end;  // the block's budget end (decode_planes sets it; pos never passes it)
   uint32_t x0, x1, x2, x3, x4;
   // byte address of the row holding bit p: lds32 + 256 * (p >> 5), in two
   // instructions (the compiler's form of the same expression takes three)

@@ -1351,14 +1351,19 @@ ZFP_HD PW decode_plane_lut(unsigned& bits, unsigned& n, Reader& rd, bool& slow) 
   return lut_finish<DIMS, PW>(bits, n, rd, slow, nf, m, w, e1, e2);
 }
 
-// The 3D decoder's plane step.  n is kept at most N-1 (with n = N-1 the group
-// part is the last position's bit alone, looked up in two dedicated entries),
-// so the verbatim mask is one shift.  Common case: the code ends within the
-// two chunks, below position N-1 (one wave-uniform test covers both).
+// The decoder's plane step.  The reader holds the block's budget as an end
+// position (rd.end: the read position never passes it), so the common path
+// clips its advance with one min and keeps no separate bit count; the rare
+// paths compute the budget left as rd.end - rd.pos.  n is kept at most N-1
+// (with n = N-1 the group part is the last position's bit alone, looked up in
+// two dedicated entries, which reads the same bits as n = N), so the window
+// offset and the verbatim mask take n as it is.  Common case: the code ends
+// within the two chunks, below position N-1 (one wave-uniform test covers
+// both).
 template <int DIMS, typename PW, typename Reader>
-ZFP_HD PW decode_plane_fast(unsigned& bits, unsigned& n, Reader& rd, bool& slow, bool& rare) {
+ZFP_HD PW decode_plane_fast(unsigned& n, Reader& rd, bool& slow, bool& rare) {
   constexpr unsigned N = 1u << (2 * DIMS);
-  const unsigned nf = n < N - 1 ? n : N - 1;
+  const unsigned nf = n;  // <= N-1
   uint64_t w;
   uint32_t g;
   rd.windows(nf, w, g);
@@ -1393,33 +1398,38 @@ ZFP_HD PW decode_plane_fast(unsigned& bits, unsigned& n, Reader& rd, bool& slow,
   // chunks) or reaches position N-1 takes, for the whole wave, the
   // budget-aware resolution from the entries already read (lut_finish);
   // `slow` is left only for the general decoder's cases.
-  if (__builtin_expect(rare, 0))
-    return lut_finish<DIMS, PW>(bits, n, rd, slow, nf, umin(nf, bits), w, e1, e2);
+  if (__builtin_expect(rare, 0)) {
+    unsigned bits = rd.end - rd.pos;
+    const PW x = lut_finish<DIMS, PW>(bits, n, rd, slow, nf, umin(nf, bits), w, e1, e2);
+    n = umin(n, N - 1);
+    return x;
+  }
   // bits >= nf of the plane from the group code, below it verbatim: one
   // v_bfi_b32 a dword under the mask ~0 << nf
   const PW x = merge_at<PW>(nf, ones, w);
   n = nf + npos;
-  const unsigned adv = umin(nf + used, bits);
 #if defined(CUZFP_EXP_DEC_EXTRA_RT)  // timing experiment: one more dependent LDS round trip a plane
   {
-    uint32_t a = adv;
-    const uint32_t dummy = rd.window32(rd.pos + adv);
-    asm volatile("; dep %1" : "+v"(a) : "v"(dummy));  // adv waits for the read
-    rd.pos += a;
+    uint32_t a = nf + used;
+    const uint32_t dummy = rd.window32(rd.pos + a);
+    asm volatile("; dep %1" : "+v"(a) : "v"(dummy));  // the advance waits for the read
+    rd.pos = umin(rd.pos + a, rd.end);
   }
 #else
-  rd.pos += adv;
+  rd.pos = umin(rd.pos + nf + used, rd.end);
 #endif
-  bits -= adv;
   return x;
 }
 
 // Plane loop: the table decoder for every lane, then, only when some lane of
-// the wave needs it, the general decoder for those lanes.
+// the wave needs it, the general decoder for those lanes.  (n <= N-1 in and
+// out.)
 template <int DIMS, typename PW, typename Reader>
-ZFP_HD PW decode_plane_any(unsigned& bits, unsigned& n, Reader& rd) {
+ZFP_HD PW decode_plane_any(unsigned& n, Reader& rd) {
+  constexpr unsigned N = 1u << (2 * DIMS);
   const auto pos0 = rd.pos;
-  const unsigned n0 = n, bits0 = bits;
+  const unsigned n0 = n;
+  unsigned bits = rd.end - pos0;
   bool slow;
   PW x = decode_plane_lut<DIMS, PW>(bits, n, rd, slow);
   ZFP_COUNT_PATH(slow ? 6 : 5);
@@ -1427,10 +1437,11 @@ ZFP_HD PW decode_plane_any(unsigned& bits, unsigned& n, Reader& rd) {
     if (slow) {
       rd.init(pos0);
       n = n0;
-      bits = bits0;
+      bits = rd.end - pos0;
       x = decode_plane<DIMS, PW>(bits, n, rd);
     }
   }
+  n = umin(n, N - 1);
   return x;
 }
 
@@ -1442,18 +1453,20 @@ ZFP_HD PW decode_plane_any(unsigned& bits, unsigned& n, Reader& rd) {
 // The fast step with the general decoder for the lanes the tables cannot finish
 // (none on the bench fields: tools/dec_paths.cpp).
 template <int DIMS, typename PW, typename Reader>
-ZFP_HD PW decode_plane_fast_any(unsigned& bits, unsigned& n, Reader& rd) {
+ZFP_HD PW decode_plane_fast_any(unsigned& n, Reader& rd) {
+  constexpr unsigned N = 1u << (2 * DIMS);
   const auto pos0 = rd.pos;
-  const unsigned n0 = n, bits0 = bits;
+  const unsigned n0 = n;
   bool slow, rare;
-  PW x = decode_plane_fast<DIMS, PW>(bits, n, rd, slow, rare);
+  PW x = decode_plane_fast<DIMS, PW>(n, rd, slow, rare);
   ZFP_COUNT_PATH(slow ? 2 : rare ? 1 : 0);
   if (__builtin_expect(rare, 0) && any_lane(slow)) {
     if (slow) {
       rd.init(pos0);
       n = n0;
-      bits = bits0;
+      unsigned bits = rd.end - pos0;
       x = decode_plane<DIMS, PW>(bits, n, rd);
+      n = umin(n, N - 1);
     }
   }
   return x;
@@ -1463,11 +1476,11 @@ ZFP_HD PW decode_plane_fast_any(unsigned& bits, unsigned& n, Reader& rd) {
 // wave has budget (a lane without deposits zeros).  Returns the highest plane
 // left unset (-1: none); those below it are unset too.
 template <int H, typename UInt, int DIMS, typename Reader>
-ZFP_HD int decode_half(planes<UInt, DIMS>& P, unsigned& bits, unsigned& n, int cmin, Reader& rd) {
+ZFP_HD int decode_half(planes<UInt, DIMS>& P, unsigned& n, int cmin, Reader& rd) {
   typedef typename plane_word<DIMS>::type PW;
   int c = 31;
   for (; c - 1 >= cmin; c -= 2) {
-    if (!any_lane(bits != 0)) return c;
+    if (!any_lane(rd.pos < rd.end)) return c;
 #if defined(CUZFP_EXP_DTRIPS)  // timing experiment: only the first CUZFP_EXP_DTRIPS trips (wrong output)
     if (c < 31 - 2 * CUZFP_EXP_DTRIPS) return c;
 #endif
@@ -1475,19 +1488,19 @@ ZFP_HD int decode_half(planes<UInt, DIMS>& P, unsigned& bits, unsigned& n, int c
       progress_priority<CUZFP_DPRIO_T2, CUZFP_DPRIO_T1, CUZFP_DPRIO_T0>(uniform(c));
     PW xa, xb;
     if constexpr (DIMS >= CUZFP_FAST_DIMS) {
-      xa = decode_plane_fast_any<DIMS, PW>(bits, n, rd);
-      xb = decode_plane_fast_any<DIMS, PW>(bits, n, rd);
+      xa = decode_plane_fast_any<DIMS, PW>(n, rd);
+      xb = decode_plane_fast_any<DIMS, PW>(n, rd);
       ZFP_STAMP(4);  // diagnostic builds: the last fast pair's end
     } else {
-      xa = decode_plane_any<DIMS, PW>(bits, n, rd);
-      xb = decode_plane_any<DIMS, PW>(bits, n, rd);
+      xa = decode_plane_any<DIMS, PW>(n, rd);
+      xb = decode_plane_any<DIMS, PW>(n, rd);
     }
     const int u = uniform(c);
     P.template set<H>(u, xa);
     P.template set<H>(u - 1, xb);
   }
-  if (c >= cmin && c >= 0 && any_lane(bits != 0)) {
-    P.template set<H>(uniform(c), decode_plane_any<DIMS, PW>(bits, n, rd));
+  if (c >= cmin && c >= 0 && any_lane(rd.pos < rd.end)) {
+    P.template set<H>(uniform(c), decode_plane_any<DIMS, PW>(n, rd));
     c--;
   }
   return c;
@@ -1499,10 +1512,10 @@ ZFP_HD int decode_half(planes<UInt, DIMS>& P, unsigned& bits, unsigned& n, int c
 // the priority drops sit at fixed trips.  Returns the highest plane left
 // unset (-1: none), as decode_half.
 template <int H, int C, bool PRI = true, typename UInt, int DIMS, typename Reader>
-ZFP_HD int decode_half_fixed(planes<UInt, DIMS>& P, unsigned& bits, unsigned& n, Reader& rd) {
+ZFP_HD int decode_half_fixed(planes<UInt, DIMS>& P, unsigned& n, Reader& rd) {
   typedef typename plane_word<DIMS>::type PW;
   if constexpr (C >= 1) {
-    if (!any_lane(bits != 0)) return C;
+    if (!any_lane(rd.pos < rd.end)) return C;
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(CUZFP_NO_PRIO)
     if constexpr (prio_of<Reader>::value && PRI) {
       if constexpr (C == CUZFP_DPRIO_T2) __builtin_amdgcn_s_setprio(2);
@@ -1510,12 +1523,12 @@ ZFP_HD int decode_half_fixed(planes<UInt, DIMS>& P, unsigned& bits, unsigned& n,
       else if constexpr (C == CUZFP_DPRIO_T0) __builtin_amdgcn_s_setprio(0);
     }
 #endif
-    const PW xa = decode_plane_fast_any<DIMS, PW>(bits, n, rd);
-    const PW xb = decode_plane_fast_any<DIMS, PW>(bits, n, rd);
+    const PW xa = decode_plane_fast_any<DIMS, PW>(n, rd);
+    const PW xb = decode_plane_fast_any<DIMS, PW>(n, rd);
     ZFP_STAMP(4);  // diagnostic builds: the last pair's end
     P.template set<H>(C, xa);
     P.template set<H>(C - 1, xb);
-    return decode_half_fixed<H, C - 2, PRI>(P, bits, n, rd);
+    return decode_half_fixed<H, C - 2, PRI>(P, n, rd);
   }
   return C;
 }
@@ -1541,26 +1554,27 @@ template <typename UInt, int DIMS, typename Reader>
 ZFP_HD void decode_planes(planes<UInt, DIMS>& P, unsigned budget, unsigned maxprec, Reader& rd) {
   constexpr int PREC = (int)sizeof(UInt) * 8;
   const int kmin = PREC > (int)maxprec ? PREC - (int)maxprec : 0;
-  unsigned bits = budget, n = 0;
+  unsigned n = 0;
+  rd.end = rd.pos + budget;  // the reader never passes it
   if constexpr (!(kLazyZero && DIMS == 3)) P.zero();
 #if !defined(CUZFP_DEC_LOOP)  // (CUZFP_DEC_LOOP: the rolled loop for every block, A/B builds)
   // (64-bit values keep the rolled loop: unrolled, the f64 decoder measured
   // 61.8 -> 71.2 us at 256^3 rate 16 and took minutes to compile)
   if constexpr (PREC == 32 && DIMS >= CUZFP_FAST_DIMS) {
     if (!any_lane(kmin != 0)) {  // every lane decodes down to plane 0 (normal floats)
-      zero_planes<0>(P, decode_half_fixed<0, 31>(P, bits, n, rd));
+      zero_planes<0>(P, decode_half_fixed<0, 31>(P, n, rd));
       return;
     }
   }
 #endif
   if constexpr (PREC == 64) {
-    zero_planes<1>(P, decode_half<1>(P, bits, n, kmin > 32 ? kmin - 32 : 0, rd));
+    zero_planes<1>(P, decode_half<1>(P, n, kmin > 32 ? kmin - 32 : 0, rd));
     if (kmin >= 32) {
       zero_planes<0>(P, 31);
       return;
     }
   }
-  zero_planes<0>(P, decode_half<0>(P, bits, n, kmin, rd));
+  zero_planes<0>(P, decode_half<0>(P, n, kmin, rd));
 }
 
 // ---------------------------------------------------------------------------

@@ -133,28 +133,30 @@ extern "C" long long emu_fuzz_plane(unsigned long long seed, long long trials, i
     const unsigned bits0 = (unsigned)(rnd() % 161);  // 0: a lane whose block is done (it keeps stepping with its wave)
     const size_t end = bits0;  // the budget ends where the block does
     HostReader ra{buf, 6, 0, end}, rb{buf, 6, 0, end};
-    unsigned na = n0, ba = bits0, nb = n0, bb = bits0;
-    uint64_t xa, xb;
-    if (dims == 3) {
-      xa = cuzfp::decode_plane_any<3, uint64_t>(ba, na, ra);
-      xb = cuzfp::decode_plane<3, uint64_t>(bb, nb, rb);
-    } else if (dims == 2) {
-      xa = cuzfp::decode_plane_any<2, uint32_t>(ba, na, ra);
-      xb = cuzfp::decode_plane<2, uint32_t>(bb, nb, rb);
-    } else {
-      xa = cuzfp::decode_plane_any<1, uint32_t>(ba, na, ra);
-      xb = cuzfp::decode_plane<1, uint32_t>(bb, nb, rb);
-    }
     // n = N-1 and n = N are the same state (the table steps keep n <= N-1)
     auto cap = [&](unsigned v) { return v < N - 1 ? v : N - 1; };
-    if (xa != xb || cap(na) != cap(nb) || ba != bb || ra.pos != rb.pos) bad++;
+    unsigned na = cap(n0), nb = n0, bb = bits0;
+    uint64_t xa, xb;
+    if (dims == 3) {
+      xa = cuzfp::decode_plane_any<3, uint64_t>(na, ra);
+      xb = cuzfp::decode_plane<3, uint64_t>(bb, nb, rb);
+    } else if (dims == 2) {
+      xa = cuzfp::decode_plane_any<2, uint32_t>(na, ra);
+      xb = cuzfp::decode_plane<2, uint32_t>(bb, nb, rb);
+    } else {
+      xa = cuzfp::decode_plane_any<1, uint32_t>(na, ra);
+      xb = cuzfp::decode_plane<1, uint32_t>(bb, nb, rb);
+    }
+    // the table steps keep the budget as the reader's end position: the bits
+    // left are end - pos
+    if (xa != xb || na != cap(nb) || ra.pos != rb.pos || end - rb.pos != bb) bad++;
     {  // the fast step with the budget (decode_half's every step)
       HostReader rc{buf, 6, 0, end};
-      unsigned nc = n0, bc = bits0;
-      const uint64_t xc = dims == 3 ? cuzfp::decode_plane_fast_any<3, uint64_t>(bc, nc, rc)
-                          : dims == 2 ? (uint64_t)cuzfp::decode_plane_fast_any<2, uint32_t>(bc, nc, rc)
-                                      : (uint64_t)cuzfp::decode_plane_fast_any<1, uint32_t>(bc, nc, rc);
-      if (xc != xb || cap(nc) != cap(nb) || bc != bb || rc.pos != rb.pos) bad++;
+      unsigned nc = cap(n0);
+      const uint64_t xc = dims == 3 ? cuzfp::decode_plane_fast_any<3, uint64_t>(nc, rc)
+                          : dims == 2 ? (uint64_t)cuzfp::decode_plane_fast_any<2, uint32_t>(nc, rc)
+                                      : (uint64_t)cuzfp::decode_plane_fast_any<1, uint32_t>(nc, rc);
+      if (xc != xb || nc != cap(nb) || rc.pos != rb.pos) bad++;
     }
   }
   return bad;
