@@ -69,8 +69,17 @@ constexpr size_t kChunkLutBytes = sizeof(ChunkLut);
 // (the same values to the same addresses) and waits only for its own writes,
 // so the waves need no barrier.
 __device__ const SpreadTab g_spread_tab = make_spread_tab();
+// ... and the 1D tables (zfp_block.hpp): the encoder's pair table, the
+// decoder's plane table
+__device__ const Pair1dLut g_pair1d_lut = make_pair1d_lut();
+__device__ const Plane1dDecLut g_plane1d_lut = make_plane1d_dec_lut();
 constexpr size_t kSpreadTabBytes = sizeof(SpreadTab);
 typedef __attribute__((address_space(3))) const uint32_t lds_spread;
+#if !defined(CUZFP_EXP_P1D_NOLDS)
+typedef lds_spread* P1dPtr;
+#else
+typedef const uint32_t* P1dPtr;
+#endif
 
 // ---------------------------------------------------------------------------
 // LDS bit writers / reader (one lane, one block)
@@ -90,6 +99,8 @@ struct LdsOrWriter {
   uint64_t* p;          // the lane's column: word j at p[64 j], W + kSlackWords words, zeroed
   lds_spread* lut;      // the workgroup's spread tables
   uint32_t pos, lim;    // bits produced; 64 * W
+  P1dPtr p1d;           // 1D: the workgroup's pair table (Pair1dLut)
+  __device__ __forceinline__ uint32_t pair1d(uint32_t o) const { return *(P1dPtr)((uintptr_t)p1d + o); }
 #if defined(CUZFP_EXP_NOPUT)
   uint64_t sink = 0;
 #endif
@@ -132,6 +143,8 @@ struct LdsBitWriter {
   lds_spread* lut;         // the workgroup's spread tables
   uint32_t pos, end, cnt;  // pos: stream offset of acc's bit 0
   uint64_t acc;
+  P1dPtr p1d;              // 1D: the workgroup's pair table (Pair1dLut)
+  __device__ __forceinline__ uint32_t pair1d(uint32_t o) const { return *(P1dPtr)((uintptr_t)p1d + o); }
 #if defined(CUZFP_EXP_NOPUT)
   uint64_t sink = 0;
 #endif
@@ -172,6 +185,35 @@ struct LdsBitWriter {
   __device__ __forceinline__ void settle() {}  // emit() drops bits past maxbits
 };
 
+// maxbits <= 64 (1D rate <= 16, 2D rate <= 4: BASELINE's 2D 8192^2 rate 2 and
+// 1D rate 8): the lane's whole block is one 64-bit register.  A put ORs its
+// bits in at the count; the count stops at maxbits, so a full lane's further
+// puts land at or past bit maxbits, which the kernel masks off.  With maxbits
+// = 64 (FULL64) a full lane's puts are masked to zero instead (a shift by 64
+// would wrap).  No LDS image, no flush.
+template <bool PRIO = true, bool FULL64 = false>
+struct RegWriter {
+  static constexpr bool kPrio = PRIO;
+  lds_spread* lut;  // the workgroup's spread tables
+  P1dPtr p1d;       // 1D: the pair table
+  uint64_t acc;
+  uint32_t cnt, mb;  // bits produced (at most mb); maxbits
+  __device__ __forceinline__ bool full() const { return cnt >= mb; }
+  __device__ __forceinline__ void put(uint64_t v, unsigned n) {
+    if constexpr (FULL64) v &= (uint64_t)(int64_t)((int32_t)(cnt - 64u) >> 31);  // all ones while cnt < 64
+    acc |= shl64(v, cnt);
+    cnt = umin(cnt + n, mb);
+  }
+  __device__ __forceinline__ void zero_bit() { cnt = umin(cnt + 1, mb); }
+  __device__ __forceinline__ uint32_t sp0(uint32_t o) const { return *(lds_spread*)((uintptr_t)lut + o); }
+  __device__ __forceinline__ uint32_t sp1(uint32_t o) const { return *(lds_spread*)((uintptr_t)(lut + 256) + o); }
+  __device__ __forceinline__ uint32_t spread(uint32_t b) const { return lut[256 + b] >> 1; }
+  __device__ __forceinline__ uint32_t pair1d(uint32_t o) const { return *(P1dPtr)((uintptr_t)p1d + o); }
+  __device__ __forceinline__ void finish() {}
+  __device__ __forceinline__ void settle() {}
+  __device__ __forceinline__ uint64_t bits() const { return acc & lowmask(mb); }
+};
+
 // Reader over the lane's block in the wave's lane-interleaved LDS image
 // (dword j of the block at lds32[64 * j]; pos counts bits from the block's
 // start).  The table decoder reads its windows fresh per plane; the general
@@ -186,6 +228,7 @@ struct LdsReader {
   static constexpr bool kPrio = PRIO;
   const uint32_t* lds32;
   const uint32_t* lut32;  // the workgroup's copy of the chunk tables (static LDS)
+  const uint16_t* d1d;    // 1D: the workgroup's plane table (Plane1dDecLut)
   uint32_t pos;
   uint32_t end;  // the block's budget end (decode_planes sets it; pos never passes it)
   uint32_t x0, x1, x2, x3, x4;
@@ -236,11 +279,16 @@ struct LdsReader {
   // instead of bank conflicts (random entries made 51 % of the decoder's LDS
   // cycles conflict cycles, SQ_LDS_BANK_CONFLICT)
   static __device__ __forceinline__ uint32_t lead_masked(uint32_t g) {
+#if defined(CUZFP_EXP_NOLEAD)  // A/B: unmasked (more bank conflicts, two VALU fewer)
+    return g;
+#endif
     uint32_t t;
     asm("v_bfe_i32 %0, %1, 0, 1" : "=v"(t) : "v"(g));
     return g & t;
   }
-  // byte offsets of chunk 1 (bits 0-9) and chunk 2 (bits 10-19) in a state's table
+  // byte offsets of chunk 1's state-2 entry (chunk bits 0-9; the state-2
+  // table is at LDS address 0) and of chunk 2's pair of state-0/1 entries
+  // (bits 10-19; from the pair table's start, kLutPairs)
   static __device__ __forceinline__ uint32_t off1(uint32_t gm) {
     uint32_t a;
     asm("v_lshlrev_b32 %0, 2, %1\n\tv_and_b32 %0, 0xffc, %0" : "=&v"(a) : "v"(gm));
@@ -248,14 +296,23 @@ struct LdsReader {
   }
   static __device__ __forceinline__ uint32_t off2(uint32_t gm) {
     uint32_t a;
-    asm("v_lshrrev_b32 %0, 8, %1\n\tv_and_b32 %0, 0xffc, %0" : "=&v"(a) : "v"(gm));
+    asm("v_lshrrev_b32 %0, 7, %1\n\tv_and_b32 %0, 0x1ff8, %0" : "=&v"(a) : "v"(gm));
     return a;
   }
-  static constexpr uint32_t kStateBytes = 4u << kChunkBits;  // one state's table
-  // the table steps' lookups: entry (2, g's chunk 1) and entries (0, chunk 2),
-  // (1, chunk 2).  (With n = N-1 the group part is the last position's bit
-  // alone; the parse then runs past position N-1, which the steps' implied-one
-  // rule resolves.)
+  static constexpr uint32_t kPairBytes = 4u * kLutPairs;  // byte address of the pair table
+  typedef __attribute__((address_space(3))) const uint64_t lds_u64;
+  __device__ __forceinline__ uint2 tab64(uint32_t byte_off) const {
+#if defined(CUZFP_EXP_GTAB)
+    const uint64_t v = *(const uint64_t*)((const char*)g_chunk_lut.e + byte_off);
+#else
+    const uint64_t v = *(lds_u64*)((uintptr_t)(lds_u32*)lut32 + byte_off);
+#endif
+    return uint2{(uint32_t)v, (uint32_t)(v >> 32)};
+  }
+  // the table steps' lookups: entry (2, g's chunk 1) and the pair (0, chunk 2),
+  // (1, chunk 2) in one ds_read_b64.  (With n = N-1 the group part is the last
+  // position's bit alone; the parse then runs past position N-1, which the
+  // steps' implied-one rule resolves.)
   __device__ __forceinline__ void chunks_fast(uint32_t g, uint32_t& e1, uint32_t& e2a, uint32_t& e2b) const {
 #if defined(CUZFP_EXP_DEC_NOLUT)  // timing experiment: no table reads (short ended codes), wrong output
     e1 = pack_entry(g & 0x3ffu, ((g >> 10) & 7u) + 1u, ((g >> 13) & 7u) + 1u, 0);
@@ -263,10 +320,10 @@ struct LdsReader {
     return;
 #endif
     const uint32_t gm = lead_masked(g);
-    const uint32_t a2 = off2(gm);
-    e1 = tab(2 * kStateBytes + off1(gm));
-    e2a = tab(a2);
-    e2b = tab(kStateBytes + a2);
+    e1 = tab(off1(gm));
+    const uint2 p = tab64(kPairBytes + off2(gm));
+    e2a = p.x;
+    e2b = p.y;
   }
   // continuation pairs (dense planes): 32 stream bits at bit q of the block,
   // chunk A in state st (0/1), chunk B in states 0 and 1
@@ -276,14 +333,18 @@ struct LdsReader {
   }
   __device__ __forceinline__ void chunks_st(uint32_t g, uint32_t st, uint32_t& eA, uint32_t& eBa,
                                             uint32_t& eBb) const {
-    const uint32_t a2 = off2(g);
-    eA = tab((st << 12) + off1(g));
-    eBa = tab(a2);
-    eBb = tab(kStateBytes + a2);
+    eA = tab(kPairBytes + ((g << 3) & 0x1ff8u) + 4u * st);
+    const uint2 p = tab64(kPairBytes + off2(g));
+    eBa = p.x;
+    eBb = p.y;
   }
   __device__ __forceinline__ uint32_t chunk1_fast(uint32_t g) const {
-    return tab(2 * kStateBytes + off1(lead_masked(g)));
+    return tab(off1(lead_masked(g)));
   }
+  // 1D: an entry of the plane table (o: byte offset) and the 8 stream bits at pos
+  typedef __attribute__((address_space(3))) const uint16_t lds_u16;
+  __device__ __forceinline__ uint32_t dec1d(uint32_t o) const { return *(lds_u16*)((uintptr_t)(lds_u16*)d1d + o); }
+  __device__ __forceinline__ uint32_t bits8() const { return window32(pos) & 0xffu; }
   __device__ __forceinline__ void load() {
     const uint32_t* r = lds32 + (pos >> 5) * 64;
     x0 = r[0];
@@ -329,6 +390,7 @@ struct RegReader : LdsReader<PRIO> {
   }
   __device__ __forceinline__ uint64_t peek() const { return at(this->pos); }
   __device__ __forceinline__ uint32_t window32(uint32_t q) const { return (uint32_t)at(q); }
+  __device__ __forceinline__ uint32_t bits8() const { return (uint32_t)(blk >> (this->pos & 63)) & 0xffu; }
   __device__ __forceinline__ void peek2(uint64_t& a, uint64_t& b) const {
     a = at(this->pos);
     b = 0;  // bits past 64: past the block
@@ -512,6 +574,15 @@ __device__ __forceinline__ void scatter(Scalar* __restrict__ data, const Geometr
 // synchronise with each other.  Within a wave, LDS traffic between lanes only
 // needs the wave's own LDS operations to have completed.
 constexpr int kWavesPerGroup = 4;
+// Workgroup size of the 1D register-reader decoder: 16 waves, so that the
+// workgroup's 20 KiB of tables are shared by 16 waves that each decode 1 KiB
+// of values (64M values: decode 151 -> 121 us).  The 2D decoder and the 1D/2D
+// register-writer encoders measured best at 4 (16: 2D encode 66.6 -> 71.3
+// us, 1D 97 -> 102 us; 2D decode unchanged).
+#ifndef CUZFP_REG_WAVES_1D  // A/B builds
+#define CUZFP_REG_WAVES_1D 16
+#endif
+constexpr int kRegWaves1d = CUZFP_REG_WAVES_1D;
 
 __device__ __forceinline__ void wave_lds_sync() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -531,12 +602,17 @@ template <typename Scalar, int DIMS, bool ENC = false> struct occupancy {
   static constexpr int value = (sizeof(Scalar) == 8 && DIMS == 3) ? (ENC ? CUZFP_F64_ENC_WAVES : 2) : 4;
 };
 
-template <typename Scalar, int DIMS, bool FAST, bool ALIGNED, bool PRIO = true>
-__global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS, true>::value)) void zfp_encode(const Scalar* __restrict__ data,
+// REG (1D/2D, maxbits 32 or 64): the block is coded into a register
+// (RegWriter; 2 = maxbits 64) and stored straight from it: a lane's block is
+// dword / word b of the stream.  No LDS image.
+template <typename Scalar, int DIMS, bool FAST, bool ALIGNED, bool PRIO = true, int REG = 0, int WPG = kWavesPerGroup>
+__global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS, true>::value)) void zfp_encode(const Scalar* __restrict__ data,
                                                                       Geometry g,
                                                                       uint64_t* __restrict__ stream) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds_all[];
   __shared__ __attribute__((aligned(16))) uint32_t stab[512];  // LDS address 0 (static)
+  // 1D: the pair table (Pair1dLut, 4 KiB), one copy a workgroup: 16 bytes a lane
+  __shared__ __attribute__((aligned(16))) uint32_t ptab[DIMS == 1 ? 1024 : 4];
   constexpr int N = 1 << (2 * DIMS);
   const uint32_t wig = threadIdx.x >> 6;  // wave in workgroup
   const uint32_t wave = g.wave0 + blockIdx.x * (blockDim.x >> 6) + wig;
@@ -544,17 +620,37 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS, t
   const uint32_t b = wave * kLanes + lane;
   const bool live_wave = wave < g.wave_end;
   uint64_t* lds = lds_all + (size_t)wig * g.lds_words;
+  // the register-path kernels (1D/2D) copy the spread tables once a workgroup
+  constexpr bool kGroupSpread = DIMS == 1 || REG != 0;
+  if constexpr (DIMS == 2 && REG != 0) {
+    for (uint32_t i = threadIdx.x; i < kSpreadTabBytes / 16; i += blockDim.x)
+      ((uint4*)stab)[i] = ((const uint4*)g_spread_tab.e)[i];
+    __syncthreads();
+  }
+  if constexpr (DIMS == 1) {
+    // ... and the 64 bytes of spread table 1D reads (entries 0-15 of table 0:
+    // r = x >> n < 2^4), behind the same barrier
+    if (threadIdx.x < 4) ((uint4*)stab)[threadIdx.x] = ((const uint4*)g_spread_tab.e)[threadIdx.x];
+#if !defined(CUZFP_EXP_P1D_NOLDS)
+    for (uint32_t i = threadIdx.x; i < sizeof(Pair1dLut) / 16; i += blockDim.x)
+      ((uint4*)ptab)[i] = ((const uint4*)g_pair1d_lut.e)[i];
+#endif
+    __syncthreads();
+  }
+#if !defined(CUZFP_EXP_P1D_NOLDS)
+  lds_spread* p1d = (lds_spread*)ptab;
+#else  // timing experiment: the pair table read through the vector caches, no LDS copy
+  const uint32_t* p1d = g_pair1d_lut.e;
+#endif
   if (!live_wave) return;
   // the plane coder's spread tables, written whole by every wave (see
   // g_spread_tab): their load is issued first so that storing them waits only
   // for it, not for the block's gathers
   constexpr uint32_t kTabPieces = kSpreadTabBytes / 16;  // two 16-byte pieces a lane
+  // (1D: copied above, per workgroup; a per-lane staging array here was turned
+  // into LDS by the compiler and made the 1D register-writer kernel 8x slower)
   uint4 tab16[kTabPieces / kLanes];
-  // (1D reads entries 0-15 of table 0 alone: r = x >> n < 2^4, so lanes 0-3
-  // copy 64 bytes instead of the whole 2 KiB)
-  if constexpr (DIMS == 1) {
-    if (lane < 4) tab16[0] = ((const uint4*)g_spread_tab.e)[lane];
-  } else {
+  if constexpr (!kGroupSpread) {
 #pragma unroll
     for (uint32_t i = 0; i < kTabPieces / kLanes; i++) tab16[i] = ((const uint4*)g_spread_tab.e)[lane + i * kLanes];
   }
@@ -599,25 +695,41 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS, t
   if (b < g.nblocks) gather<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
 #endif
   // (one copy a workgroup behind a barrier measured slower: 28.0 -> 28.4 us at 256^3)
-  if constexpr (DIMS == 1) {
-    if (lane < 4) ((uint4*)stab)[lane] = tab16[0];
-  } else {
+  if constexpr (!kGroupSpread) {
 #pragma unroll
     for (uint32_t i = 0; i < kTabPieces / kLanes; i++) ((uint4*)stab)[lane + i * kLanes] = tab16[i];
   }
 #if defined(CUZFP_EXP_PAD) && defined(__HIP_DEVICE_COMPILE__) && CUZFP_EXP_PAD_AT == 0
   exp_pad(lane);  // timing experiment: dummy VALU work while the gathers are in flight
 #endif
+  if constexpr (REG) {
+    wave_lds_sync();  // the spread tables
+    uint64_t bits = 0;
+    if (b < g.nblocks) {
+      RegWriter<PRIO, REG == 2> wr{lut, p1d, 0, 0, g.maxbits};
+      encode_block<Scalar, DIMS>(f, g.maxbits, wr);
+      bits = wr.bits();
+    }
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);
+    // block b is dword (maxbits 32) / word (64) b; with maxbits 32 and an odd
+    // block count the lane after the last block writes the last word's zero half
+    if constexpr (REG == 2) {
+      if (b < g.nblocks) stream[b] = bits;
+    } else {
+      if (b < g.nblocks + (g.nblocks & 1u)) ((uint32_t*)stream)[b] = (uint32_t)bits;
+    }
+    return;
+  }
   if (b < g.nblocks) {
     if constexpr (ALIGNED) {
       uint64_t* mine = lds + lane;
       for (uint32_t j = 0; j < W + kSlackWords; j++) mine[j * 64] = 0;  // own column
       wave_lds_sync();  // the tables
-      LdsOrWriter<PRIO> wr{mine, lut, 0, 64 * W};
+      LdsOrWriter<PRIO> wr{mine, lut, 0, 64 * W, p1d};
       encode_block<Scalar, DIMS>(f, g.maxbits, wr);
     } else {
       wave_lds_sync();  // the tables and the zeroed image
-      LdsBitWriter<PRIO> wr{lds, lut, lane * g.maxbits, (lane + 1) * g.maxbits, 0, 0};
+      LdsBitWriter<PRIO> wr{lds, lut, lane * g.maxbits, (lane + 1) * g.maxbits, 0, 0, p1d};
       encode_block<Scalar, DIMS>(f, g.maxbits, wr);
     }
   }
@@ -655,8 +767,10 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS, t
   ZFP_STAMP_REAL(9);
 }
 
-template <typename Scalar, int DIMS, bool FAST, bool PRIO = true, bool REG = false>
-__global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::value)) void zfp_decode(const uint64_t* __restrict__ stream,
+// WPG: waves per workgroup (16 for the 1D register-reader kernel, whose
+// workgroup copies 20 KiB of tables for 1 KiB of output a wave)
+template <typename Scalar, int DIMS, bool FAST, bool PRIO = true, bool REG = false, int WPG = kWavesPerGroup>
+__global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) void zfp_decode(const uint64_t* __restrict__ stream,
                                                                       Geometry g,
                                                                       Scalar* __restrict__ data) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds_all[];
@@ -675,9 +789,16 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
   // block's loads are issued first, then the workgroup's copy of the chunk
   // tables, so both latencies overlap before the one barrier.
   __shared__ __attribute__((aligned(16))) uint32_t ctab[kChunkLutBytes / 4];  // LDS address 0 (static)
+  // 1D: the plane table (Plane1dDecLut, 16 KiB)
+  __shared__ __attribute__((aligned(16))) uint16_t dtab[DIMS == 1 ? sizeof(Plane1dDecLut) / 2 : 8];
   uint32_t* lut = ctab;
-  // (1D reads chunk-1 entries only: state 2 and the no-group entry)
-  constexpr uint32_t kLutFrom = DIMS == 1 ? (2u << kChunkBits) / 4 : 0;
+  auto copy_dtab = [&]() {
+    if constexpr (DIMS == 1)
+      for (uint32_t i = threadIdx.x; i < sizeof(Plane1dDecLut) / 16; i += blockDim.x)
+        ((uint4*)dtab)[i] = ((const uint4*)g_plane1d_lut.e)[i];
+  };
+  // (1D reads chunk-1 entries only: the state-2 table, the first kLutPairs entries)
+  constexpr uint32_t kLutEnd = DIMS == 1 ? kLutPairs * 4 / 16 : sizeof(ChunkLut) / 16;
   const uint32_t* seg = (const uint32_t*)(stream + (size_t)wave * g.maxbits);
   uint32_t* L = (uint32_t*)lds + lane;
   uint64_t blk = 0;
@@ -695,9 +816,10 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
              ((uint64_t)__builtin_amdgcn_alignbit(a2, a1, s0) << 32)) & lowmask(g.maxbits);
     }
 #if !defined(CUZFP_EXP_GTAB)
-    for (uint32_t i = kLutFrom + threadIdx.x; i < sizeof(ChunkLut) / 16; i += blockDim.x)
+    for (uint32_t i = threadIdx.x; i < kLutEnd; i += blockDim.x)
       ((uint4*)lut)[i] = ((const uint4*)g_chunk_lut.e)[i];
 #endif
+    copy_dtab();
   } else {
     const uint32_t D = (g.maxbits + 31) >> 5;  // dwords per block
     const bool vec = (g.maxbits & 127) == 0 && g.vec_io;
@@ -709,8 +831,9 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
       for (uint32_t q = 0; q < kHeld; q++)
         if (4 * q < D) held[q] = ld16<kNtStream>(&src[q]);
     }
-    for (uint32_t i = kLutFrom + threadIdx.x; i < sizeof(ChunkLut) / 16; i += blockDim.x)
+    for (uint32_t i = threadIdx.x; i < kLutEnd; i += blockDim.x)
       ((uint4*)lut)[i] = ((const uint4*)g_chunk_lut.e)[i];
+    copy_dtab();
     if (live) {
       if (vec) {
 #pragma unroll
@@ -763,6 +886,7 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
       RegReader<PRIO> rd;
       rd.lds32 = L;
       rd.lut32 = lut;
+      rd.d1d = dtab;
       rd.blk = blk;
       rd.init(0);
       coded = decode_block<Scalar, DIMS>(f, g.maxbits, rd);
@@ -770,6 +894,7 @@ __global__ __launch_bounds__(kLanes * kWavesPerGroup, (occupancy<Scalar, DIMS>::
       LdsReader<PRIO> rd;
       rd.lds32 = L;
       rd.lut32 = lut;
+      rd.d1d = dtab;
       rd.init(0);
       coded = decode_block<Scalar, DIMS>(f, g.maxbits, rd);
     }
@@ -855,6 +980,14 @@ static inline bool use_priority(uint32_t nwaves, int waves_per_simd, uint32_t ro
   return nwaves <= (uint32_t)c * 4u * (uint32_t)waves_per_simd * rounds;
 }
 
+#if defined(CUZFP_EXP_NOREG)  // A/B builds: no register-writer encoder
+constexpr bool kExpNoReg = true;
+#else
+constexpr bool kExpNoReg = false;
+#endif
+#ifndef CUZFP_ENC_PRIO_ROUNDS  // A/B builds: 0 = the encoder never takes the schedule
+#define CUZFP_ENC_PRIO_ROUNDS 1
+#endif
 template <typename Scalar, int DIMS>
 int launch_encode_t(const void* data, const Geometry& g, bool fast, uint64_t* stream,
                            uint32_t wave0, uint32_t nwaves, hipStream_t st) {
@@ -863,16 +996,40 @@ int launch_encode_t(const void* data, const Geometry& g, bool fast, uint64_t* st
   gg.wave_end = wave0 + nwaves;
   gg.vec_io = (g.maxbits % 2 == 0) && ((uintptr_t)stream % 16 == 0);
   gg.lds_words = g.maxbits + kLanes * kSlackWords;  // + per-lane slack
+  // the kernel's static LDS: the spread tables, and in 1D the pair table
+  constexpr size_t kStatic = kSpreadTabBytes + (DIMS == 1 ? sizeof(Pair1dLut) : 16);
+  const Scalar* d = (const Scalar*)data;
+  if constexpr (DIMS <= 2 && !kExpNoReg) {
+    // maxbits 32 or 64: the register writer, blocks stored straight from it
+    if (g.maxbits == 32 || g.maxbits == 64) {
+      gg.lds_words = 0;
+      const dim3 grid((nwaves + kWavesPerGroup - 1) / kWavesPerGroup), block(kLanes * kWavesPerGroup);
+      const bool prio = use_priority(nwaves, occupancy<Scalar, DIMS, true>::value, CUZFP_ENC_PRIO_ROUNDS);
+#define ZFP_ENC_REG(FAST_, PRIO_)                                                                          \
+  do {                                                                                                     \
+    if (g.maxbits == 64)                                                                                   \
+      hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, FAST_, true, PRIO_, 2>), grid, block, 0, st, d, gg, stream); \
+    else                                                                                                   \
+      hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, FAST_, true, PRIO_, 1>), grid, block, 0, st, d, gg, stream); \
+  } while (0)
+      if (fast && prio) ZFP_ENC_REG(true, true);
+      else if (fast) ZFP_ENC_REG(true, false);
+      else if (prio) ZFP_ENC_REG(false, true);
+      else ZFP_ENC_REG(false, false);
+#undef ZFP_ENC_REG
+      const hipError_t e = hipGetLastError();
+      t_last_hip = e;
+      return e == hipSuccess ? CUZFP_SUCCESS : CUZFP_ERROR_HIP;
+    }
+  }
   // the word-aligned writer pads each lane with slack words; very large maxbits
   // (whose padded image would pass the workgroup's LDS) take the general writer
-  const bool aligned = (g.maxbits & 63) == 0 && gg.lds_words * 8 + kSpreadTabBytes <= lds_cap_bytes();
+  const bool aligned = (g.maxbits & 63) == 0 && gg.lds_words * 8 + kStatic <= lds_cap_bytes();
   if (!aligned) gg.lds_words = g.maxbits + 2;
-  // (the spread tables are the kernel's static LDS, kSpreadTabBytes a workgroup)
-  const uint32_t wpg = waves_per_group(gg.lds_words, kSpreadTabBytes);
+  const uint32_t wpg = waves_per_group(gg.lds_words, kStatic);
   const dim3 grid((nwaves + wpg - 1) / wpg), block(kLanes * wpg);
   const size_t lds = (size_t)wpg * gg.lds_words * 8;
-  const Scalar* d = (const Scalar*)data;
-  if (fast && aligned && !use_priority(nwaves, occupancy<Scalar, DIMS, true>::value, 1))
+  if (fast && aligned && !use_priority(nwaves, occupancy<Scalar, DIMS, true>::value, CUZFP_ENC_PRIO_ROUNDS))
     hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, true, true, false>), grid, block, lds, st, d, gg, stream);
   else if (fast && aligned)
     hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, true, true>), grid, block, lds, st, d, gg, stream);
@@ -905,21 +1062,23 @@ int launch_decode_t(const uint64_t* stream, const Geometry& g, bool fast, void* 
   // blocks of at most 64 bits are read into registers (RegReader): no LDS image
   const bool reg = DIMS <= 2 && g.maxbits <= 64;
   if (reg) gg.lds_words = 0;
-  const uint32_t wpg = waves_per_group(gg.lds_words, kChunkLutBytes);
+  const uint32_t wpg = waves_per_group(gg.lds_words, kChunkLutBytes + (DIMS == 1 ? sizeof(Plane1dDecLut) : 16));
   const dim3 grid((nwaves + wpg - 1) / wpg), block(kLanes * wpg);
   const size_t lds = (size_t)wpg * gg.lds_words * 8;  // (+ the static chunk tables)
   Scalar* d = (Scalar*)data;
   if constexpr (DIMS <= 2) {
     if (reg) {
       const bool prio = use_priority(nwaves, occupancy<Scalar, DIMS>::value, 2);
+      constexpr int W = DIMS == 1 ? kRegWaves1d : kWavesPerGroup;
+      const dim3 rgrid((nwaves + W - 1) / W), rblock(kLanes * W);
       if (fast && prio)
-        hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, true, true, true>), grid, block, lds, st, stream, gg, d);
+        hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, true, true, true, W>), rgrid, rblock, 0, st, stream, gg, d);
       else if (fast)
-        hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, true, false, true>), grid, block, lds, st, stream, gg, d);
+        hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, true, false, true, W>), rgrid, rblock, 0, st, stream, gg, d);
       else if (prio)
-        hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, false, true, true>), grid, block, lds, st, stream, gg, d);
+        hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, false, true, true, W>), rgrid, rblock, 0, st, stream, gg, d);
       else
-        hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, false, false, true>), grid, block, lds, st, stream, gg, d);
+        hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, false, false, true, W>), rgrid, rblock, 0, st, stream, gg, d);
       const hipError_t e = hipGetLastError();
       t_last_hip = e;
       return e == hipSuccess ? CUZFP_SUCCESS : CUZFP_ERROR_HIP;

@@ -853,11 +853,145 @@ ZFP_HD bool encode_half_fixed(const planes<UInt, DIMS>& P, unsigned& n, Writer& 
   return true;
 }
 
+// ---------------------------------------------------------------------------
+// 1D blocks by table (4 coefficients: a plane is a nibble).
+//
+// Encoder: one lookup codes two planes.  Entry (n, a, b) -- n the count of
+// significant coefficients before plane a (kept at most N-1 = 3, see
+// encode_plane_one_put), a and b the two planes' nibbles -- holds the two plane
+// codes concatenated (at most 2 x 7 bits), their length and the n after plane
+// b.  The codes are those of encode.c:121-151 without a budget: the writer
+// drops what passes the block's maxbits, and the reference writes exactly the
+// budget's prefix of the same bits.
+//
+// Decoder: one lookup decodes one plane, budget included.  Entry (n, c, s) --
+// c = min(bits left, 7) (a 1D plane code has at most 7 bits, so c = 7 means
+// "not cut"), s the next 8 stream bits -- holds the plane's nibble, the bits
+// read and the n after it, from decode.c:288-321 run on those bits with that
+// budget (its quirk -- a one deposited where the budget ends a run of zeros --
+// included).  So the 1D plane loop has no rare path and no branch on the data.
+
+// encode.c:136-150 for one 1D plane x (4 bits) with n significant: the code's
+// bits (LSB first), their count, and n afterwards
+constexpr void plane_code_1d(uint32_t x, uint32_t& n, uint32_t& code, uint32_t& len) {
+  constexpr uint32_t N = 4;
+  code = 0;
+  len = 0;
+  for (uint32_t i = 0; i < n; i++) code |= ((x >> i) & 1u) << len++;
+  x >>= n;
+  while (n < N) {
+    const uint32_t t = x ? 1u : 0u;  // group test
+    code |= t << len++;
+    if (!t) break;
+    while (n < N - 1) {  // the run up to the next one (the one at N-1 is implied)
+      const uint32_t b = x & 1u;
+      code |= b << len++;
+      if (b) break;
+      x >>= 1;
+      n++;
+    }
+    x >>= 1;
+    n++;
+  }
+}
+struct Pair1dLut {
+  uint32_t e[4 * 256];  // [n][a << 4 | b]: code [0,14) | length << 14 | n' << 30
+};
+constexpr Pair1dLut make_pair1d_lut() {
+  Pair1dLut t{};
+  for (uint32_t n0 = 0; n0 < 4; n0++)
+    for (uint32_t ab = 0; ab < 256; ab++) {
+      uint32_t n = n0, ca = 0, la = 0, cb = 0, lb = 0;
+      plane_code_1d(ab >> 4, n, ca, la);
+      n = n < 3 ? n : 3;
+      plane_code_1d(ab & 15u, n, cb, lb);
+      n = n < 3 ? n : 3;
+      t.e[n0 * 256 + ab] = (ca | (cb << la)) | ((la + lb) << 14) | (n << 30);
+    }
+  return t;
+}
+// byte offset of the (n, a, b) entry, n given as n << 10
+ZFP_HD uint32_t pair1d_off(uint32_t n10, uint32_t a, uint32_t b) { return n10 | (a << 6) | (b << 2); }
+
+// decode.c:288-321 for one 1D plane: the stream bits s (LSB first), budget c
+constexpr void plane_decode_1d(uint32_t s, uint32_t c, uint32_t& n, uint32_t& x, uint32_t& used) {
+  constexpr uint32_t N = 4;
+  uint32_t bits = c, p = 0;
+  const uint32_t m = n < bits ? n : bits;
+  x = s & ((1u << m) - 1u);
+  p = m;
+  bits -= m;
+  while (n < N && bits) {
+    bits--;
+    if (!((s >> p++) & 1u)) break;  // group test "0"
+    while (n < N - 1 && bits) {
+      bits--;
+      if ((s >> p++) & 1u) break;  // the one
+      n++;
+    }
+    x += 1u << n;
+    n++;
+  }
+  used = c - bits;
+}
+struct Plane1dDecLut {
+  uint16_t e[4 * 8 * 256];  // [n][c][s]: nibble | used << 4 | n' << 8
+};
+constexpr Plane1dDecLut make_plane1d_dec_lut() {
+  Plane1dDecLut t{};
+  for (uint32_t n0 = 0; n0 < 4; n0++)
+    for (uint32_t c = 0; c < 8; c++)
+      for (uint32_t s = 0; s < 256; s++) {
+        uint32_t n = n0, x = 0, used = 0;
+        plane_decode_1d(s, c, n, x, used);
+        n = n < 3 ? n : 3;
+        t.e[(n0 * 8 + c) * 256 + s] = (uint16_t)(x | (used << 4) | (n << 8));
+      }
+  return t;
+}
+
+// Writers that hold the 1D pair table (pair1d(byte offset) reads an entry)
+template <typename T, typename = void> struct has_pair1d {
+  static constexpr bool value = false;
+};
+template <typename T> struct has_pair1d<T, decltype((void)&T::pair1d)> {
+  static constexpr bool value = true;
+};
+
+// Planes C, C-1, ... 1, 0 of 32-bit half H of a 1D block, two per lookup,
+// while any lane of the wave has budget; false once every lane is full.
+template <int H, int C, typename UInt, typename Writer>
+ZFP_HD bool encode_pairs_1d(const planes<UInt, 1>& P, uint32_t& n10, Writer& wr) {
+  if constexpr (C >= 1) {
+    if (!any_lane(!wr.full())) return false;
+    constexpr int S = 4 * (C / 4);  // planes C and C-1 share a nibble position (C odd)
+    const uint32_t a = (P.v[H][0][C % 4] >> S) & 15u, b = (P.v[H][0][(C - 1) % 4] >> S) & 15u;
+    const uint32_t e = wr.pair1d(pair1d_off(n10, a, b));
+    wr.put(e & 0x3fffu, (e >> 14) & 31u);
+    n10 = (e >> 20) & 0xc00u;
+    return encode_pairs_1d<H, C - 2>(P, n10, wr);
+  }
+  return true;
+}
+
 template <typename UInt, int DIMS, typename Writer>
 ZFP_HD void encode_planes(const planes<UInt, DIMS>& P, unsigned maxprec, Writer& wr) {
   constexpr int PREC = (int)sizeof(UInt) * 8;
   const int kmin = PREC > (int)maxprec ? PREC - (int)maxprec : 0;
   unsigned n = 0;
+#if defined(CUZFP_EXP_NOPAIR1D)  // A/B builds: the 1D plane steps without the pair table
+  if constexpr (false) {
+#else
+  if constexpr (DIMS == 1 && has_pair1d<Writer>::value) {
+#endif
+    if (!any_lane(kmin != 0)) {  // every lane codes down to plane 0
+      uint32_t n10 = 0;
+      if constexpr (PREC == 64)
+        if (!encode_pairs_1d<1, 31>(P, n10, wr)) return;
+      encode_pairs_1d<0, 31>(P, n10, wr);
+      return;
+    }
+  }
 #if !defined(CUZFP_ENC_LOOP)  // (CUZFP_ENC_LOOP: the rolled loop below for every block, A/B builds)
   if (!any_lane(kmin != 0)) {  // every lane codes down to plane 0 (normal floats)
     if constexpr (PREC == 32) {
@@ -1120,13 +1254,25 @@ constexpr uint32_t chunk_entry(unsigned state, uint32_t b) {
   return pack_entry(ones, pos, kChunkBits + mark_open, 0);
 }
 
+// Table layout: state 2 (chunk 1, the leading group test first) at
+// [0, 2^B), indexed by the chunk; states 0 and 1 side by side at
+// [2^B, 2^B + 2^(B+1)), chunk b's pair at 2^B + 2b, so one ds_read_b64 reads
+// both (64 banks, one LDS instruction, where two ds_read_b32 -- or one
+// ds_read2st64_b32, served as two -- each take the 32-bank conflicts of the
+// lanes' random entries).  1D reads the state-2 table alone.
+constexpr uint32_t kLutS2 = 0, kLutPairs = 1u << kChunkBits;
+ZFP_HD constexpr uint32_t lut_s2_index(uint32_t b) { return kLutS2 + (b & kChunkMask); }
+ZFP_HD constexpr uint32_t lut_pair_index(uint32_t b, uint32_t state) { return kLutPairs + 2u * (b & kChunkMask) + state; }
 struct ChunkLut {
-  uint32_t e[3u << kChunkBits];  // [state][chunk]
+  uint32_t e[3u << kChunkBits];
 };
 constexpr ChunkLut make_chunk_lut() {
   ChunkLut t{};
-  for (unsigned s = 0; s < 3; s++)
-    for (uint32_t b = 0; b <= kChunkMask; b++) t.e[(s << kChunkBits) | b] = chunk_entry(s, b);
+  for (uint32_t b = 0; b <= kChunkMask; b++) {
+    t.e[lut_s2_index(b)] = chunk_entry(2, b);
+    t.e[lut_pair_index(b, 0)] = chunk_entry(0, b);
+    t.e[lut_pair_index(b, 1)] = chunk_entry(1, b);
+  }
   return t;
 }
 
@@ -1550,6 +1696,34 @@ ZFP_HD void zero_planes(planes<UInt, DIMS>& P, int c) {
     for (; c >= 0; c--) P.template set<H>(uniform(c), 0);
 }
 
+// Readers that hold the 1D plane table (dec1d(byte offset) reads an entry,
+// bits8() the next 8 stream bits, zeros past the block)
+template <typename T, typename = void> struct has_dec1d {
+  static constexpr bool value = false;
+};
+template <typename T> struct has_dec1d<T, decltype((void)&T::dec1d)> {
+  static constexpr bool value = true;
+};
+
+// Planes C, C-1, ... 0 of 32-bit half H of a 1D block, one lookup each
+// (Plane1dDecLut), while any lane of the wave has budget (tested every other
+// plane; a lane without budget looks up c = 0: nothing read, nothing set).
+// n12 = n << 12, the byte offset of n's part of the table.
+template <int H, int C, typename UInt, typename Reader>
+ZFP_HD void decode_planes_1d(planes<UInt, 1>& P, uint32_t& n12, Reader& rd) {
+  if constexpr (C >= 0) {
+    if constexpr (C & 1)
+      if (!any_lane(rd.pos < rd.end)) return;
+    const uint32_t s = rd.bits8();
+    const uint32_t c = umin(rd.end - rd.pos, 7u);
+    const uint32_t e = rd.dec1d(n12 | (c << 9) | (s << 1));
+    P.v[H][0][C % 4] |= (e & 15u) << (4 * (C / 4));
+    rd.pos += (e >> 4) & 15u;
+    n12 = (e << 4) & 0x3000u;
+    decode_planes_1d<H, C - 1>(P, n12, rd);
+  }
+}
+
 template <typename UInt, int DIMS, typename Reader>
 ZFP_HD void decode_planes(planes<UInt, DIMS>& P, unsigned budget, unsigned maxprec, Reader& rd) {
   constexpr int PREC = (int)sizeof(UInt) * 8;
@@ -1557,6 +1731,14 @@ ZFP_HD void decode_planes(planes<UInt, DIMS>& P, unsigned budget, unsigned maxpr
   unsigned n = 0;
   rd.end = rd.pos + budget;  // the reader never passes it
   if constexpr (!(kLazyZero && DIMS == 3)) P.zero();
+  if constexpr (DIMS == 1 && has_dec1d<Reader>::value) {
+    if (!any_lane(kmin != 0)) {  // every lane decodes down to plane 0
+      uint32_t n12 = 0;
+      if constexpr (PREC == 64) decode_planes_1d<1, 31>(P, n12, rd);
+      decode_planes_1d<0, 31>(P, n12, rd);
+      return;
+    }
+  }
 #if !defined(CUZFP_DEC_LOOP)  // (CUZFP_DEC_LOOP: the rolled loop for every block, A/B builds)
   // (64-bit values keep the rolled loop: unrolled, the f64 decoder measured
   // 61.8 -> 71.2 us at 256^3 rate 16 and took minutes to compile)

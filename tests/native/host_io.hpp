@@ -42,6 +42,11 @@ struct HostWriter {
     static const cuzfp::SpreadTab t = cuzfp::make_spread_tab();
     return t;
   }
+  // the 1D pair table (o: byte offset)
+  uint32_t pair1d(uint32_t o) const {
+    static const cuzfp::Pair1dLut t = cuzfp::make_pair1d_lut();
+    return t.e[o >> 2];
+  }
 };
 
 struct HostReader {
@@ -72,6 +77,12 @@ struct HostReader {
     g = (uint32_t)peek();
     pos -= m;
   }
+  // the 1D plane table (o: byte offset) and the next 8 stream bits
+  uint32_t dec1d(uint32_t o) const {
+    static const cuzfp::Plane1dDecLut t = cuzfp::make_plane1d_dec_lut();
+    return t.e[o >> 1];
+  }
+  uint32_t bits8() const { return (uint32_t)peek() & 0xffu; }
   static const cuzfp::ChunkLut& table() {
     static const cuzfp::ChunkLut t = cuzfp::make_chunk_lut();
     return t;
@@ -79,15 +90,12 @@ struct HostReader {
   void chunks_fast(uint32_t g, uint32_t& e1, uint32_t& e2a, uint32_t& e2b) const {
     const uint32_t* t = table().e;
     const uint32_t gm = (g & 1u) ? g : 0u;
-    const uint32_t c2 = (gm >> cuzfp::kChunkBits) & cuzfp::kChunkMask;
-    e1 = t[(2u << cuzfp::kChunkBits) | (gm & cuzfp::kChunkMask)];
-    e2a = t[c2];
-    e2b = t[c2 + (1u << cuzfp::kChunkBits)];
+    const uint32_t c2 = gm >> cuzfp::kChunkBits;
+    e1 = t[cuzfp::lut_s2_index(gm)];
+    e2a = t[cuzfp::lut_pair_index(c2, 0)];
+    e2b = t[cuzfp::lut_pair_index(c2, 1)];
   }
-  uint32_t chunk1_fast(uint32_t g) const {
-    const uint32_t gm = (g & 1u) ? g : 0u;
-    return table().e[(2u << cuzfp::kChunkBits) | (gm & cuzfp::kChunkMask)];
-  }
+  uint32_t chunk1_fast(uint32_t g) const { return table().e[cuzfp::lut_s2_index(g)]; }
   // continuation pairs: 32 stream bits at q, chunk A in state st, chunk B in states 0 and 1
   uint32_t window32(size_t q) {
     const size_t p = pos;
@@ -98,10 +106,10 @@ struct HostReader {
   }
   void chunks_st(uint32_t g, uint32_t st, uint32_t& eA, uint32_t& eBa, uint32_t& eBb) const {
     const uint32_t* t = table().e;
-    const uint32_t c2 = (g >> cuzfp::kChunkBits) & cuzfp::kChunkMask;
-    eA = t[(st << cuzfp::kChunkBits) | (g & cuzfp::kChunkMask)];
-    eBa = t[c2];
-    eBb = t[c2 + (1u << cuzfp::kChunkBits)];
+    const uint32_t c2 = g >> cuzfp::kChunkBits;
+    eA = t[cuzfp::lut_pair_index(g, st)];
+    eBa = t[cuzfp::lut_pair_index(c2, 0)];
+    eBb = t[cuzfp::lut_pair_index(c2, 1)];
   }
 };
 

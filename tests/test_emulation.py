@@ -16,6 +16,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "tests", "native", "emulate.cpp")
 HDR = os.path.join(ROOT, "cuzfp_amd", "csrc", "zfp_block.hpp")
+HOST_IO = os.path.join(ROOT, "tests", "native", "host_io.hpp")
 LIB = os.path.join(ROOT, "build", "libcuzfp_emu.so")
 TC = {np.dtype(np.int32): 1, np.dtype(np.int64): 2, np.dtype(np.float32): 3, np.dtype(np.float64): 4}
 
@@ -23,7 +24,7 @@ TC = {np.dtype(np.int32): 1, np.dtype(np.int64): 2, np.dtype(np.float32): 3, np.
 @pytest.fixture(scope="module")
 def emu():
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
-    if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(SRC), os.path.getmtime(HDR)):
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(f) for f in (SRC, HDR, HOST_IO)):
         subprocess.check_call(["/opt/rocm/llvm/bin/clang++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wno-unknown-pragmas",
                                "-o", LIB, SRC])
     lib = ctypes.CDLL(LIB)
