@@ -367,95 +367,123 @@ ZFP_HD void transpose_tiles(uint32_t* a) {
   if constexpr (R >= 2) transpose_stage<1, INV>(a, R);
 }
 
-// Planes of N = 4^DIMS coefficients held as 32-bit words.  For 32-bit
-// coefficients W = N words; 64-bit coefficients are split into low and high
-// halves (planes 0..31 from the low words, 32..63 from the high words).
-//
-// The words live in vector registers as clang ext_vector_type values of R
-// words (v[h][g][row] = word g*R + row of half h), so the plane coders can
-// index them with a runtime, wave-uniform plane number: the compiler lowers
-// that to s_set_gpr_idx_on + v_mov (VGPR-relative addressing), which keeps the
-// plane loop a loop -- one copy of its body in the instruction cache -- instead
-// of 32 or 64 unrolled copies.  (A runtime index into a plain array, or into a
-// vector wider than 32 registers, would be lowered to scratch memory.)
-template <typename UInt, int DIMS> struct planes {
-  static constexpr int N = 1 << (2 * DIMS);
-  static constexpr int H = sizeof(UInt) / 4;      // 32-bit halves per value
-  static constexpr int R = N < 32 ? N : 32;       // tile height
-  static constexpr int G = N / R;                 // row groups (2 for 3D)
+// Storage of the plane words.  64-bit coefficients keep them as clang
+// ext_vector_type values (one R-register tuple per row group), which the
+// rolled plane loops index with a runtime, wave-uniform plane number:
+// VGPR-relative addressing (s_set_gpr_idx_on + v_mov), one copy of the loop
+// body in the instruction cache.  (A runtime index into a plain array, or
+// into a vector wider than 32 registers, would be lowered to scratch memory.
+// Unrolled with plain registers, the f64 kernels still need ~190-200 VGPRs --
+// two waves a SIMD, as rolled -- and the unit takes 14 minutes to compile.)
+// 32-bit coefficients are always coded down to plane 0 (precision() is 32 for
+// every f32 exponent and for int32), so their plane loops are unrolled with
+// compile-time plane numbers and the words are plain registers: no tuple the
+// register allocator must keep contiguous.
+template <int H, int G, int R, bool VEC> struct plane_words;
+template <int H, int G, int R> struct plane_words<H, G, R, false> {
+  uint32_t a[H][G][R];
+  ZFP_HD uint32_t get(int h, int g, int r) const { return a[h][g][r]; }
+  ZFP_HD void set(int h, int g, int r, uint32_t x) { a[h][g][r] = x; }
+  ZFP_HD void zero() {
+#pragma unroll
+    for (int h = 0; h < H; h++)
+#pragma unroll
+      for (int g = 0; g < G; g++)
+#pragma unroll
+        for (int r = 0; r < R; r++) a[h][g][r] = 0u;
+  }
+};
+template <int H, int G, int R> struct plane_words<H, G, R, true> {
   typedef uint32_t vec __attribute__((ext_vector_type(R)));
   vec v[H][G];
-
-  // NEG_ODD: u holds q + 0xaaaa... and the planes get the negabinary's
-  // final "^ 0xaaaa..." (the odd planes inverted) from the transpose
-  template <bool NEG_ODD = false>
-  ZFP_HD void load(const UInt* u) {
-    uint32_t w[H][N];
-#pragma unroll
-    for (int i = 0; i < N; i++) {
-      w[0][i] = (uint32_t)u[i];
-      if (H == 2) w[H - 1][i] = (uint32_t)((uint64_t)u[i] >> 32);
-    }
-#pragma unroll
-    for (int h = 0; h < H; h++)
-#pragma unroll
-      for (int g = 0; g < G; g++) transpose_tiles<R, NEG_ODD ? kOddWords : kInvNone>(&w[h][g * R]);
-#pragma unroll
-    for (int h = 0; h < H; h++)
-#pragma unroll
-      for (int g = 0; g < G; g++)
-#pragma unroll
-        for (int r = 0; r < R; r++) v[h][g][r] = w[h][g * R + r];
-  }
-
-  // NEG_ODD: the coefficients come out as u ^ 0xaaaa... (the first half of
-  // the inverse negabinary conversion)
-  template <bool NEG_ODD = false>
-  ZFP_HD void store(UInt* u) const {
-    uint32_t w[H][N];
-#pragma unroll
-    for (int h = 0; h < H; h++)
-#pragma unroll
-      for (int g = 0; g < G; g++)
-#pragma unroll
-        for (int r = 0; r < R; r++) w[h][g * R + r] = v[h][g][r];
-#pragma unroll
-    for (int h = 0; h < H; h++)
-#pragma unroll
-      for (int g = 0; g < G; g++) transpose_tiles<R, NEG_ODD ? kOddBits : kInvNone>(&w[h][g * R]);
-#pragma unroll
-    for (int i = 0; i < N; i++) {
-      uint64_t x = w[0][i];
-      if (H == 2) x |= (uint64_t)w[H - 1][i] << 32;
-      u[i] = (UInt)x;
-    }
-  }
-
+  ZFP_HD uint32_t get(int h, int g, int r) const { return v[h][g][r]; }
+  ZFP_HD void set(int h, int g, int r, uint32_t x) { v[h][g][r] = x; }
   ZFP_HD void zero() {
 #pragma unroll
     for (int h = 0; h < H; h++)
 #pragma unroll
       for (int g = 0; g < G; g++) v[h][g] = (vec)0u;
   }
+};
+
+// Planes of N = 4^DIMS coefficients held as 32-bit words.  For 32-bit
+// coefficients W = N words; 64-bit coefficients are split into low and high
+// halves (planes 0..31 from the low words, 32..63 from the high words).
+// Word (h, g, row) = word g*R + row of half h.
+template <typename UInt, int DIMS> struct planes {
+  static constexpr int N = 1 << (2 * DIMS);
+  static constexpr int H = sizeof(UInt) / 4;      // 32-bit halves per value
+  static constexpr int R = N < 32 ? N : 32;       // tile height
+  static constexpr int G = N / R;                 // row groups (2 for 3D)
+  plane_words<H, G, R, (H == 2)> w;
+
+  // NEG_ODD: u holds q + 0xaaaa... and the planes get the negabinary's
+  // final "^ 0xaaaa..." (the odd planes inverted) from the transpose
+  template <bool NEG_ODD = false>
+  ZFP_HD void load(const UInt* u) {
+    uint32_t t[H][N];
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      t[0][i] = (uint32_t)u[i];
+      if (H == 2) t[H - 1][i] = (uint32_t)((uint64_t)u[i] >> 32);
+    }
+#pragma unroll
+    for (int h = 0; h < H; h++)
+#pragma unroll
+      for (int g = 0; g < G; g++) transpose_tiles<R, NEG_ODD ? kOddWords : kInvNone>(&t[h][g * R]);
+#pragma unroll
+    for (int h = 0; h < H; h++)
+#pragma unroll
+      for (int g = 0; g < G; g++)
+#pragma unroll
+        for (int r = 0; r < R; r++) w.set(h, g, r, t[h][g * R + r]);
+  }
+
+  // NEG_ODD: the coefficients come out as u ^ 0xaaaa... (the first half of
+  // the inverse negabinary conversion)
+  template <bool NEG_ODD = false>
+  ZFP_HD void store(UInt* u) const {
+    uint32_t t[H][N];
+#pragma unroll
+    for (int h = 0; h < H; h++)
+#pragma unroll
+      for (int g = 0; g < G; g++)
+#pragma unroll
+        for (int r = 0; r < R; r++) t[h][g * R + r] = w.get(h, g, r);
+#pragma unroll
+    for (int h = 0; h < H; h++)
+#pragma unroll
+      for (int g = 0; g < G; g++) transpose_tiles<R, NEG_ODD ? kOddBits : kInvNone>(&t[h][g * R]);
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      uint64_t x = t[0][i];
+      if (H == 2) x |= (uint64_t)t[H - 1][i] << 32;
+      u[i] = (UInt)x;
+    }
+  }
+
+  ZFP_HD void zero() { w.zero(); }
 
   // plane c (0..31) of half h as an N-bit word (bit i = that bit of
   // coefficient i); h is a compile-time constant, c may be a runtime value
-  // (wave-uniform in the kernels).
+  // (wave-uniform in the kernels) for 64-bit coefficients only.
   template <int h> ZFP_HD uint64_t get(int c) const {
-    if constexpr (N == 64) return (uint64_t)v[h][0][c] | ((uint64_t)v[h][1][c] << 32);
-    else return (v[h][0][c % R] >> (R * (c / R))) & (uint32_t)lowmask(R);
+    if constexpr (N == 64) return (uint64_t)w.get(h, 0, c) | ((uint64_t)w.get(h, 1, c) << 32);
+    else return (w.get(h, 0, c % R) >> (R * (c / R))) & (uint32_t)lowmask(R);
   }
   ZFP_HD uint64_t get(int k) const {  // k compile-time after unrolling
     return (k >> 5) ? get<H - 1>(k & 31) : get<0>(k & 31);
   }
+  // the word holding plane c of half h (1D/2D: with R planes a word)
+  template <int h> ZFP_HD uint32_t word(int c) const { return w.get(h, 0, c % R); }
 
   // deposit plane c of half h (bits beyond N are zero; the plane was zero)
   template <int h> ZFP_HD void set(int c, uint64_t x) {
     if constexpr (N == 64) {
-      v[h][0][c] = (uint32_t)x;
-      v[h][1][c] = (uint32_t)(x >> 32);
+      w.set(h, 0, c, (uint32_t)x);
+      w.set(h, 1, c, (uint32_t)(x >> 32));
     } else {
-      v[h][0][c % R] |= (uint32_t)x << (R * (c / R));
+      w.set(h, 0, c % R, w.get(h, 0, c % R) | ((uint32_t)x << (R * (c / R))));
     }
   }
   ZFP_HD void set(int k, uint64_t x) {
@@ -965,7 +993,7 @@ ZFP_HD bool encode_pairs_1d(const planes<UInt, 1>& P, uint32_t& n10, Writer& wr)
   if constexpr (C >= 1) {
     if (!any_lane(!wr.full())) return false;
     constexpr int S = 4 * (C / 4);  // planes C and C-1 share a nibble position (C odd)
-    const uint32_t a = (P.v[H][0][C % 4] >> S) & 15u, b = (P.v[H][0][(C - 1) % 4] >> S) & 15u;
+    const uint32_t a = (P.template word<H>(C) >> S) & 15u, b = (P.template word<H>(C - 1) >> S) & 15u;
     const uint32_t e = wr.pair1d(pair1d_off(n10, a, b));
     wr.put(e & 0x3fffu, (e >> 14) & 31u);
     n10 = (e >> 20) & 0xc00u;
@@ -977,35 +1005,34 @@ ZFP_HD bool encode_pairs_1d(const planes<UInt, 1>& P, uint32_t& n10, Writer& wr)
 template <typename UInt, int DIMS, typename Writer>
 ZFP_HD void encode_planes(const planes<UInt, DIMS>& P, unsigned maxprec, Writer& wr) {
   constexpr int PREC = (int)sizeof(UInt) * 8;
-  const int kmin = PREC > (int)maxprec ? PREC - (int)maxprec : 0;
   unsigned n = 0;
-#if defined(CUZFP_EXP_NOPAIR1D)  // A/B builds: the 1D plane steps without the pair table
-  if constexpr (false) {
-#else
-  if constexpr (DIMS == 1 && has_pair1d<Writer>::value) {
-#endif
-    if (!any_lane(kmin != 0)) {  // every lane codes down to plane 0
+  if constexpr (PREC == 32) {
+    // 32-bit coefficients are coded down to plane 0: precision() is 32 for
+    // every f32 exponent (emax >= -149), and int32 has maxprec 32
+    (void)maxprec;
+#if !defined(CUZFP_EXP_NOPAIR1D)  // (A/B builds: the 1D plane steps without the pair table)
+    if constexpr (DIMS == 1 && has_pair1d<Writer>::value) {
       uint32_t n10 = 0;
-      if constexpr (PREC == 64)
-        if (!encode_pairs_1d<1, 31>(P, n10, wr)) return;
       encode_pairs_1d<0, 31>(P, n10, wr);
       return;
     }
-  }
-#if !defined(CUZFP_ENC_LOOP)  // (CUZFP_ENC_LOOP: the rolled loop below for every block, A/B builds)
-  if (!any_lane(kmin != 0)) {  // every lane codes down to plane 0 (normal floats)
-    if constexpr (PREC == 32) {
-      encode_half_fixed<0, 31>(P, n, wr);
-    } else {  // the priority schedule over the high half only
-      if (encode_half_fixed<1, 31>(P, n, wr)) encode_half_fixed<0, 31, false>(P, n, wr);
-    }
-    return;
-  }
 #endif
-  if constexpr (PREC == 64) {
+    encode_half_fixed<0, 31>(P, n, wr);
+  } else {
+    const int kmin = PREC > (int)maxprec ? PREC - (int)maxprec : 0;
+    if (!any_lane(kmin != 0)) {  // every lane codes down to plane 0 (normal doubles)
+      if constexpr (DIMS == 1 && has_pair1d<Writer>::value) {
+        uint32_t n10 = 0;
+        if (encode_pairs_1d<1, 31>(P, n10, wr)) encode_pairs_1d<0, 31>(P, n10, wr);
+        return;
+      }
+      // the priority schedule over the high half only
+      if (encode_half_fixed<1, 31>(P, n, wr)) encode_half_fixed<0, 31, false>(P, n, wr);
+      return;
+    }
     if (!encode_half<1>(P, n, kmin > 32 ? kmin - 32 : 0, wr)) return;
+    encode_half<0>(P, n, kmin, wr);
   }
-  encode_half<0>(P, n, kmin, wr);
 }
 
 // Decoder plane step (decode.c:288-321).
@@ -1657,11 +1684,36 @@ ZFP_HD int decode_half(planes<UInt, DIMS>& P, unsigned& n, int cmin, Reader& rd)
 // (no VGPR-relative or compare-select writes of a runtime plane number) and
 // the priority drops sit at fixed trips.  Returns the highest plane left
 // unset (-1: none), as decode_half.
+// Planes left unset by the loop must read as zero.  In 3D (set() assigns a
+// whole plane) only those are zeroed, after the loop; zeroing the whole array
+// before it costs ~90 moves a wave (the compiler then also shuffles the array
+// into the layout its indexed moves use).  1D/2D planes share registers and
+// set() ORs, so that array is zeroed up front.  (CUZFP_EAGER_ZERO: zero up
+// front in 3D too.)
+#ifndef CUZFP_EAGER_ZERO
+constexpr bool kLazyZero = true;
+#else
+constexpr bool kLazyZero = false;
+#endif
+// planes C .. 0 of half H set to zero (compile-time plane numbers)
+template <int H, int C, typename UInt, int DIMS>
+ZFP_HD void zero_fixed(planes<UInt, DIMS>& P) {
+  if constexpr (C >= 0) {
+    P.template set<H>(C, 0);
+    zero_fixed<H, C - 1>(P);
+  }
+}
+
 template <int H, int C, bool PRI = true, typename UInt, int DIMS, typename Reader>
 ZFP_HD int decode_half_fixed(planes<UInt, DIMS>& P, unsigned& n, Reader& rd) {
   typedef typename plane_word<DIMS>::type PW;
   if constexpr (C >= 1) {
-    if (!any_lane(rd.pos < rd.end)) return C;
+    if (!any_lane(rd.pos < rd.end)) {
+      // the planes left: zero in 3D (set() assigns whole words there; 1D/2D
+      // words were zeroed up front)
+      if constexpr (kLazyZero && DIMS == 3) zero_fixed<H, C>(P);
+      return C;
+    }
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(CUZFP_NO_PRIO)
     if constexpr (prio_of<Reader>::value && PRI) {
       if constexpr (C == CUZFP_DPRIO_T2) __builtin_amdgcn_s_setprio(2);
@@ -1679,17 +1731,7 @@ ZFP_HD int decode_half_fixed(planes<UInt, DIMS>& P, unsigned& n, Reader& rd) {
   return C;
 }
 
-// Planes left unset by the loop must read as zero.  In 3D (set() assigns a
-// whole plane) only those are zeroed, after the loop; zeroing the whole array
-// before it costs ~90 moves a wave (the compiler then also shuffles the array
-// into the layout its indexed moves use).  1D/2D planes share registers and
-// set() ORs, so that array is zeroed up front.  (CUZFP_EAGER_ZERO: zero up
-// front in 3D too.)
-#ifndef CUZFP_EAGER_ZERO
-constexpr bool kLazyZero = true;
-#else
-constexpr bool kLazyZero = false;
-#endif
+
 template <int H, typename UInt, int DIMS>
 ZFP_HD void zero_planes(planes<UInt, DIMS>& P, int c) {
   if constexpr (kLazyZero && DIMS == 3)
@@ -1717,7 +1759,7 @@ ZFP_HD void decode_planes_1d(planes<UInt, 1>& P, uint32_t& n12, Reader& rd) {
     const uint32_t s = rd.bits8();
     const uint32_t c = umin(rd.end - rd.pos, 7u);
     const uint32_t e = rd.dec1d(n12 | (c << 9) | (s << 1));
-    P.v[H][0][C % 4] |= (e & 15u) << (4 * (C / 4));
+    P.template set<H>(C, e & 15u);
     rd.pos += (e >> 4) & 15u;
     n12 = (e << 4) & 0x3000u;
     decode_planes_1d<H, C - 1>(P, n12, rd);
@@ -1727,36 +1769,38 @@ ZFP_HD void decode_planes_1d(planes<UInt, 1>& P, uint32_t& n12, Reader& rd) {
 template <typename UInt, int DIMS, typename Reader>
 ZFP_HD void decode_planes(planes<UInt, DIMS>& P, unsigned budget, unsigned maxprec, Reader& rd) {
   constexpr int PREC = (int)sizeof(UInt) * 8;
-  const int kmin = PREC > (int)maxprec ? PREC - (int)maxprec : 0;
   unsigned n = 0;
   rd.end = rd.pos + budget;  // the reader never passes it
   if constexpr (!(kLazyZero && DIMS == 3)) P.zero();
-  if constexpr (DIMS == 1 && has_dec1d<Reader>::value) {
-    if (!any_lane(kmin != 0)) {  // every lane decodes down to plane 0
+  if constexpr (PREC == 32) {
+    // every plane down to 0 (see encode_planes); the early exits of the
+    // unrolled loop zero what they leave
+    (void)maxprec;
+    if constexpr (DIMS == 1 && has_dec1d<Reader>::value) {
       uint32_t n12 = 0;
-      if constexpr (PREC == 64) decode_planes_1d<1, 31>(P, n12, rd);
       decode_planes_1d<0, 31>(P, n12, rd);
       return;
     }
-  }
-#if !defined(CUZFP_DEC_LOOP)  // (CUZFP_DEC_LOOP: the rolled loop for every block, A/B builds)
-  // (64-bit values keep the rolled loop: unrolled, the f64 decoder measured
-  // 61.8 -> 71.2 us at 256^3 rate 16 and took minutes to compile)
-  if constexpr (PREC == 32 && DIMS >= CUZFP_FAST_DIMS) {
-    if (!any_lane(kmin != 0)) {  // every lane decodes down to plane 0 (normal floats)
-      zero_planes<0>(P, decode_half_fixed<0, 31>(P, n, rd));
-      return;
+    decode_half_fixed<0, 31>(P, n, rd);
+  } else {
+    const int kmin = PREC > (int)maxprec ? PREC - (int)maxprec : 0;
+    if constexpr (DIMS == 1 && has_dec1d<Reader>::value) {
+      if (!any_lane(kmin != 0)) {  // every lane decodes down to plane 0
+        uint32_t n12 = 0;
+        decode_planes_1d<1, 31>(P, n12, rd);
+        decode_planes_1d<0, 31>(P, n12, rd);
+        return;
+      }
     }
-  }
-#endif
-  if constexpr (PREC == 64) {
+    // (64-bit values keep the rolled loop: unrolled, the f64 decoder measured
+    // 61.8 -> 71.2 us at 256^3 rate 16 and took minutes to compile)
     zero_planes<1>(P, decode_half<1>(P, n, kmin > 32 ? kmin - 32 : 0, rd));
     if (kmin >= 32) {
       zero_planes<0>(P, 31);
       return;
     }
+    zero_planes<0>(P, decode_half<0>(P, n, kmin, rd));
   }
-  zero_planes<0>(P, decode_half<0>(P, n, kmin, rd));
 }
 
 // ---------------------------------------------------------------------------
