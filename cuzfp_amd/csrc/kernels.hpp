@@ -574,6 +574,20 @@ __device__ __forceinline__ void scatter(Scalar* __restrict__ data, const Geometr
 // synchronise with each other.  Within a wave, LDS traffic between lanes only
 // needs the wave's own LDS operations to have completed.
 constexpr int kWavesPerGroup = 4;
+// The LDS-image kernels' workgroups (the 3D paths).  Alone, the encoder
+// measured best at 1-2 waves a workgroup (256^3 r8 encode 27.8 -> 27.5 us)
+// and the decoder, whose workgroup shares one table copy behind a barrier, at
+// 8 (23.5 -> 23.0 us; 1-2 waves: 32-34 us) -- but the encode+decode step
+// with different sizes took 55.6-56.7 us against 50.2 us with 4 and 4: a
+// kernel whose workgroups need more wave slots per CU than the previous
+// kernel's leave starts late (tools/xvar.py e1d8 / e2d8 / e2d16).
+#ifndef CUZFP_ENC_WPG  // A/B builds
+#define CUZFP_ENC_WPG 4
+#endif
+#ifndef CUZFP_DEC_WPG
+#define CUZFP_DEC_WPG 4
+#endif
+constexpr int kEncWaves = CUZFP_ENC_WPG, kDecWaves = CUZFP_DEC_WPG;
 // Workgroup size of the 1D register-reader decoder: 16 waves, so that the
 // workgroup's 20 KiB of tables are shared by 16 waves that each decode 1 KiB
 // of values (64M values: decode 151 -> 121 us).  The 2D decoder and the 1D/2D
@@ -605,7 +619,7 @@ template <typename Scalar, int DIMS, bool ENC = false> struct occupancy {
 // REG (1D/2D, maxbits 32 or 64): the block is coded into a register
 // (RegWriter; 2 = maxbits 64) and stored straight from it: a lane's block is
 // dword / word b of the stream.  No LDS image.
-template <typename Scalar, int DIMS, bool FAST, bool ALIGNED, bool PRIO = true, int REG = 0, int WPG = kWavesPerGroup>
+template <typename Scalar, int DIMS, bool FAST, bool ALIGNED, bool PRIO = true, int REG = 0, int WPG = kEncWaves>
 __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS, true>::value)) void zfp_encode(const Scalar* __restrict__ data,
                                                                       Geometry g,
                                                                       uint64_t* __restrict__ stream) {
@@ -769,7 +783,7 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS, true>::value
 
 // WPG: waves per workgroup (16 for the 1D register-reader kernel, whose
 // workgroup copies 20 KiB of tables for 1 KiB of output a wave)
-template <typename Scalar, int DIMS, bool FAST, bool PRIO = true, bool REG = false, int WPG = kWavesPerGroup>
+template <typename Scalar, int DIMS, bool FAST, bool PRIO = true, bool REG = false, int WPG = kDecWaves>
 __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) void zfp_decode(const uint64_t* __restrict__ stream,
                                                                       Geometry g,
                                                                       Scalar* __restrict__ data) {
@@ -943,10 +957,10 @@ static inline size_t lds_cap_bytes() {
   return (size_t)c;
 }
 
-// waves per workgroup: as many as fit a workgroup's LDS budget (up to 4)
-static inline uint32_t waves_per_group(uint32_t lds_words, size_t shared_bytes = 0) {
+// waves per workgroup: as many as fit a workgroup's LDS budget (up to most)
+static inline uint32_t waves_per_group(uint32_t lds_words, size_t shared_bytes, uint32_t most) {
   const size_t cap = lds_cap_bytes();
-  uint32_t w = kWavesPerGroup;
+  uint32_t w = most;
   while (w > 1 && (size_t)w * lds_words * 8 + shared_bytes > cap) w >>= 1;
   return w;
 }
@@ -1008,9 +1022,9 @@ int launch_encode_t(const void* data, const Geometry& g, bool fast, uint64_t* st
 #define ZFP_ENC_REG(FAST_, PRIO_)                                                                          \
   do {                                                                                                     \
     if (g.maxbits == 64)                                                                                   \
-      hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, FAST_, true, PRIO_, 2>), grid, block, 0, st, d, gg, stream); \
+      hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, FAST_, true, PRIO_, 2, kWavesPerGroup>), grid, block, 0, st, d, gg, stream); \
     else                                                                                                   \
-      hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, FAST_, true, PRIO_, 1>), grid, block, 0, st, d, gg, stream); \
+      hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, FAST_, true, PRIO_, 1, kWavesPerGroup>), grid, block, 0, st, d, gg, stream); \
   } while (0)
       if (fast && prio) ZFP_ENC_REG(true, true);
       else if (fast) ZFP_ENC_REG(true, false);
@@ -1026,7 +1040,7 @@ int launch_encode_t(const void* data, const Geometry& g, bool fast, uint64_t* st
   // (whose padded image would pass the workgroup's LDS) take the general writer
   const bool aligned = (g.maxbits & 63) == 0 && gg.lds_words * 8 + kStatic <= lds_cap_bytes();
   if (!aligned) gg.lds_words = g.maxbits + 2;
-  const uint32_t wpg = waves_per_group(gg.lds_words, kStatic);
+  const uint32_t wpg = waves_per_group(gg.lds_words, kStatic, kEncWaves);
   const dim3 grid((nwaves + wpg - 1) / wpg), block(kLanes * wpg);
   const size_t lds = (size_t)wpg * gg.lds_words * 8;
   if (fast && aligned && !use_priority(nwaves, occupancy<Scalar, DIMS, true>::value, CUZFP_ENC_PRIO_ROUNDS))
@@ -1062,7 +1076,7 @@ int launch_decode_t(const uint64_t* stream, const Geometry& g, bool fast, void* 
   // blocks of at most 64 bits are read into registers (RegReader): no LDS image
   const bool reg = DIMS <= 2 && g.maxbits <= 64;
   if (reg) gg.lds_words = 0;
-  const uint32_t wpg = waves_per_group(gg.lds_words, kChunkLutBytes + (DIMS == 1 ? sizeof(Plane1dDecLut) : 16));
+  const uint32_t wpg = waves_per_group(gg.lds_words, kChunkLutBytes + (DIMS == 1 ? sizeof(Plane1dDecLut) : 16), kDecWaves);
   const dim3 grid((nwaves + wpg - 1) / wpg), block(kLanes * wpg);
   const size_t lds = (size_t)wpg * gg.lds_words * 8;  // (+ the static chunk tables)
   Scalar* d = (Scalar*)data;
