@@ -597,6 +597,40 @@ constexpr int kEncWaves = CUZFP_ENC_WPG, kDecWaves = CUZFP_DEC_WPG;
 #define CUZFP_REG_WAVES_1D 16
 #endif
 constexpr int kRegWaves1d = CUZFP_REG_WAVES_1D;
+#ifndef CUZFP_REG_WAVES_2D  // A/B builds
+#define CUZFP_REG_WAVES_2D 4
+#endif
+constexpr int kRegWaves2d = CUZFP_REG_WAVES_2D;
+// 1D batches: a wave of the register-path kernels codes K batches of 64
+// blocks (zfp_encode_regk / zfp_decode_regk), so that it has K times the bytes
+// in flight -- 1D waves are small (16-24 VGPRs) and 8 a SIMD is the hardware's
+// cap -- and the decoder's workgroup copies its 20 KiB of tables once for
+// W x K batches.  64M values, rate 8 (tools/xvar.py): encode 97.2 -> 79.6 us
+// at K = 2 (4 equal, 8 spills), decode 120.3 -> 103.7 us at K = 4 with
+// 8-wave workgroups (K = 4 in 16-wave or 4-wave groups 111.5, K = 8 110).
+// 2D measured slower both ways (its waves are 34-62 VGPRs and move 4 KiB of
+// values each: encode 67.5 -> 76-77 us, decode 73.6 -> 75.3 / 83.1 us), so 2D
+// stays at one batch.  Used from kRegBatchMinWaves logical waves up: at 4M
+// values (16,384 waves) the batches measured slower (step 18.9 -> 20.3 us), at
+// 16M faster (62.8 -> 58.6 us), at 1M much slower (7.9 -> 12.4 us: idle CUs).
+#ifndef CUZFP_REG_DEC_BATCH_1D  // A/B builds (1 = off)
+#define CUZFP_REG_DEC_BATCH_1D 4
+#endif
+#ifndef CUZFP_REG_ENC_BATCH_1D
+#define CUZFP_REG_ENC_BATCH_1D 2
+#endif
+#ifndef CUZFP_REG_BATCH_WAVES_1D  // workgroup size of the batched 1D decoder
+#define CUZFP_REG_BATCH_WAVES_1D 8
+#endif
+#ifndef CUZFP_REG_BATCH_MIN_WAVES
+#define CUZFP_REG_BATCH_MIN_WAVES 32768
+#endif
+constexpr int kRegDecBatch1d = CUZFP_REG_DEC_BATCH_1D, kRegEncBatch1d = CUZFP_REG_ENC_BATCH_1D;
+constexpr int kRegBatchWaves1d = CUZFP_REG_BATCH_WAVES_1D;
+constexpr uint32_t kRegBatchMinWaves = CUZFP_REG_BATCH_MIN_WAVES;
+#ifndef CUZFP_REG_BATCH_PRIO
+#define CUZFP_REG_BATCH_PRIO 0
+#endif
 
 __device__ __forceinline__ void wave_lds_sync() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -934,6 +968,128 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) voi
   ZFP_STAMP_REAL(9);
 }
 
+// The register-writer encoder (1D/2D, maxbits 32 / 64) with K batches of 64
+// blocks a wave: every batch's gathers are issued up front (K times the bytes
+// in flight a wave: at 8 waves a SIMD, the hardware's cap, one batch a wave
+// leaves HBM short of requests), then the batches are coded in order.
+template <typename Scalar, int DIMS, bool PRIO, int REG, int WPG, int K>
+__global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS, true>::value)) void zfp_encode_regk(
+    const Scalar* __restrict__ data, Geometry g, uint64_t* __restrict__ stream) {
+  static_assert(DIMS <= 2 && (REG == 1 || REG == 2) && K >= 2 && K <= 8, "register-writer batches: 1D/2D");
+  constexpr int N = 1 << (2 * DIMS);
+  __shared__ __attribute__((aligned(16))) uint32_t stab[512];  // LDS address 0 (static)
+  __shared__ __attribute__((aligned(16))) uint32_t ptab[DIMS == 1 ? 1024 : 4];
+  const uint32_t wig = threadIdx.x >> 6;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t w0 = g.wave0 + (blockIdx.x * WPG + wig) * K;
+  Scalar f[K][N];
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    const uint32_t b = (w0 + k) * kLanes + lane;
+    if (w0 + k < g.wave_end && b < g.nblocks) gather<Scalar, DIMS, true>(data, g, block_pos<DIMS>(g, b), f[k]);
+  }
+  if constexpr (DIMS == 2) {
+    for (uint32_t i = threadIdx.x; i < kSpreadTabBytes / 16; i += blockDim.x)
+      ((uint4*)stab)[i] = ((const uint4*)g_spread_tab.e)[i];
+  } else {
+    if (threadIdx.x < 4) ((uint4*)stab)[threadIdx.x] = ((const uint4*)g_spread_tab.e)[threadIdx.x];
+    for (uint32_t i = threadIdx.x; i < sizeof(Pair1dLut) / 16; i += blockDim.x)
+      ((uint4*)ptab)[i] = ((const uint4*)g_pair1d_lut.e)[i];
+  }
+  __syncthreads();
+  lds_spread* lut = (lds_spread*)stab;
+  lds_spread* p1d = (lds_spread*)ptab;
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    const uint32_t b = (w0 + k) * kLanes + lane;
+    if (w0 + k >= g.wave_end) break;
+    uint64_t bits = 0;
+    if (b < g.nblocks) {
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);
+      RegWriter<PRIO, REG == 2> wr{lut, p1d, 0, 0, g.maxbits};
+      encode_block<Scalar, DIMS>(f[k], g.maxbits, wr);
+      bits = wr.bits();
+    }
+    // block b is dword (maxbits 32) / word (64) b; with maxbits 32 and an odd
+    // block count the lane after the last block writes the last word's zero half
+    if constexpr (REG == 2) {
+      if (b < g.nblocks) stream[b] = bits;
+    } else {
+      if (b < g.nblocks + (g.nblocks & 1u)) ((uint32_t*)stream)[b] = (uint32_t)bits;
+    }
+  }
+}
+
+// The register-reader decoder (1D/2D blocks of at most 64 bits) with K
+// batches of 64 blocks a wave: the K batches' stream words are loaded up
+// front, so a wave waits once for its loads (and once for its workgroup's
+// table copy), and each batch's stores drain while the next batch decodes.
+// Batches are taken in order, one at a time (a rolled loop: the decoder body
+// is not replicated).  Logical wave w = g.wave0 + (physical wave) * K + k.
+__device__ __forceinline__ uint64_t reg_block(const uint64_t* stream, const Geometry& g, uint32_t wave,
+                                              uint32_t lane) {
+  // bits [s0, s0 + maxbits) of the wave's segment; dwords past its last one
+  // read as zero
+  const uint32_t* seg = (const uint32_t*)(stream + (size_t)wave * g.maxbits);
+  const uint32_t nb = min((uint32_t)kLanes, g.nblocks - wave * kLanes);
+  const uint32_t lim = ((nb * g.maxbits + 63) >> 6) * 2;
+  const uint32_t s0 = lane * g.maxbits, d0 = s0 >> 5;
+  const uint32_t a0 = seg[d0];
+  const uint32_t a1 = d0 + 1 < lim ? seg[d0 + 1] : 0u;
+  const uint32_t a2 = d0 + 2 < lim ? seg[d0 + 2] : 0u;
+  return ((uint64_t)__builtin_amdgcn_alignbit(a1, a0, s0) | ((uint64_t)__builtin_amdgcn_alignbit(a2, a1, s0) << 32)) &
+         lowmask(g.maxbits);
+}
+
+template <typename Scalar, int DIMS, bool FAST, bool PRIO, int WPG, int K>
+__global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) void zfp_decode_regk(
+    const uint64_t* __restrict__ stream, Geometry g, Scalar* __restrict__ data) {
+  static_assert(DIMS <= 2 && K >= 2 && K <= 8, "register-reader batches: 1D/2D, 2-8 a wave");
+  constexpr int N = 1 << (2 * DIMS);
+  __shared__ __attribute__((aligned(16))) uint32_t ctab[kChunkLutBytes / 4];  // LDS address 0 (static)
+  __shared__ __attribute__((aligned(16))) uint16_t dtab[DIMS == 1 ? sizeof(Plane1dDecLut) / 2 : 8];
+  const uint32_t wig = threadIdx.x >> 6;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t w0 = g.wave0 + (blockIdx.x * WPG + wig) * K;
+  uint64_t q[K];
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    const uint32_t w = w0 + k;
+    q[k] = (w < g.wave_end && w * kLanes + lane < g.nblocks) ? reg_block(stream, g, w, lane) : 0ull;
+  }
+  constexpr uint32_t kLutEnd = DIMS == 1 ? kLutPairs * 4 / 16 : sizeof(ChunkLut) / 16;
+  for (uint32_t i = threadIdx.x; i < kLutEnd; i += blockDim.x) ((uint4*)ctab)[i] = ((const uint4*)g_chunk_lut.e)[i];
+  if constexpr (DIMS == 1)
+    for (uint32_t i = threadIdx.x; i < sizeof(Plane1dDecLut) / 16; i += blockDim.x)
+      ((uint4*)dtab)[i] = ((const uint4*)g_plane1d_lut.e)[i];
+  __syncthreads();
+  const uint32_t nw = w0 < g.wave_end ? min((uint32_t)K, g.wave_end - w0) : 0u;
+#pragma unroll 1
+  for (uint32_t k = 0; k < nw; k++) {
+    const uint64_t blk = q[0];
+#pragma unroll
+    for (int j = 0; j + 1 < K; j++) q[j] = q[j + 1];  // the next batch's words move up (static registers)
+    const uint32_t b = (w0 + k) * kLanes + lane;
+    if (b < g.nblocks) {
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);  // lowered through the plane loop (progress_priority)
+      Scalar f[N];
+      RegReader<PRIO> rd;
+      rd.lds32 = nullptr;
+      rd.lut32 = ctab;
+      rd.d1d = dtab;
+      rd.blk = blk;
+      rd.init(0);
+      const bool coded = decode_block<Scalar, DIMS>(f, g.maxbits, rd);
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);
+      if (!coded) {
+#pragma unroll
+        for (int i = 0; i < N; i++) f[i] = (Scalar)0;
+      }
+      scatter<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Launchers
 
@@ -1026,6 +1182,20 @@ int launch_encode_t(const void* data, const Geometry& g, bool fast, uint64_t* st
     else                                                                                                   \
       hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, FAST_, true, PRIO_, 1, kWavesPerGroup>), grid, block, 0, st, d, gg, stream); \
   } while (0)
+      if constexpr (DIMS == 1 && kRegEncBatch1d > 1) {
+        if (fast && nwaves >= kRegBatchMinWaves) {
+          constexpr int W = kWavesPerGroup, K = kRegEncBatch1d;
+          const uint32_t phys = (nwaves + K - 1) / K;
+          const dim3 kgrid((phys + W - 1) / W), kblock(kLanes * W);
+          if (g.maxbits == 64)
+            hipLaunchKernelGGL((zfp_encode_regk<Scalar, DIMS, false, 2, W, K>), kgrid, kblock, 0, st, d, gg, stream);
+          else
+            hipLaunchKernelGGL((zfp_encode_regk<Scalar, DIMS, false, 1, W, K>), kgrid, kblock, 0, st, d, gg, stream);
+          const hipError_t e = hipGetLastError();
+          t_last_hip = e;
+          return e == hipSuccess ? CUZFP_SUCCESS : CUZFP_ERROR_HIP;
+        }
+      }
       if (fast && prio) ZFP_ENC_REG(true, true);
       else if (fast) ZFP_ENC_REG(true, false);
       else if (prio) ZFP_ENC_REG(false, true);
@@ -1083,7 +1253,21 @@ int launch_decode_t(const uint64_t* stream, const Geometry& g, bool fast, void* 
   if constexpr (DIMS <= 2) {
     if (reg) {
       const bool prio = use_priority(nwaves, occupancy<Scalar, DIMS>::value, 2);
-      constexpr int W = DIMS == 1 ? kRegWaves1d : kWavesPerGroup;
+      if constexpr (DIMS == 1 && kRegDecBatch1d > 1) {
+        if (fast && nwaves >= kRegBatchMinWaves) {
+          constexpr int W = kRegBatchWaves1d, K = kRegDecBatch1d;
+          const uint32_t phys = (nwaves + K - 1) / K;
+          const dim3 kgrid((phys + W - 1) / W), kblock(kLanes * W);
+          if (CUZFP_REG_BATCH_PRIO)
+            hipLaunchKernelGGL((zfp_decode_regk<Scalar, DIMS, true, true, W, K>), kgrid, kblock, 0, st, stream, gg, d);
+          else
+            hipLaunchKernelGGL((zfp_decode_regk<Scalar, DIMS, true, false, W, K>), kgrid, kblock, 0, st, stream, gg, d);
+          const hipError_t e = hipGetLastError();
+          t_last_hip = e;
+          return e == hipSuccess ? CUZFP_SUCCESS : CUZFP_ERROR_HIP;
+        }
+      }
+      constexpr int W = DIMS == 1 ? kRegWaves1d : kRegWaves2d;
       const dim3 rgrid((nwaves + W - 1) / W), rblock(kLanes * W);
       if (fast && prio)
         hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, true, true, true, W>), rgrid, rblock, 0, st, stream, gg, d);

@@ -361,6 +361,24 @@ def test_register_reader(cuda, restatement, dims, dtype):
             assert np.array_equal(y.view(np.uint8), restatement.decompress(ref, shape, dtype, mb).view(np.uint8)), mb
 
 
+@pytest.mark.parametrize("nblocks", [64 * 32771, 64 * 32769 + 25, 64 * 32768 - 1])
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_batched_1d_waves(cuda, restatement, nblocks, dtype):
+    """1D launches of >= 32,768 waves take the batched register-path kernels
+    (kernels.hpp zfp_encode_regk / zfp_decode_regk: 2 and 4 batches of 64 blocks
+    a wave): a last wave group with fewer batches, a partial last batch, and the
+    size just below the switch (the one-batch kernels)."""
+    rng = np.random.default_rng(nblocks % 1000)
+    shape = (4 * nblocks,)
+    a = _fields(rng, shape, dtype, "smooth")
+    for rate in (3, 8, 16):
+        mb = cz.rate_to_maxbits(rate, dtype, 1)
+        words, y = _gpu_roundtrip(a, mb, cuda)
+        ref = restatement.compress(a, mb)
+        assert np.array_equal(words, ref), rate
+        assert np.array_equal(y.view(np.uint8), restatement.decompress(ref, shape, dtype, mb).view(np.uint8)), rate
+
+
 @pytest.mark.parametrize("shape,dtype,rate", [((64, 48, 40), np.float32, 8), ((24, 20, 16), np.float64, 16),
                                               ((300, 260), np.float32, 4), ((200003,), np.float32, 8)])
 @pytest.mark.parametrize("pinned", [False, True])
