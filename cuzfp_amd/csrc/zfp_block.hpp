@@ -831,6 +831,81 @@ ZFP_HD void encode_plane_step(PW x, unsigned& n, Writer& wr) {
   }
 }
 
+// Two 3D planes with one wave-uniform test: both planes' lengths first (the
+// second plane's n follows from the first's bit length alone, no table read),
+// then, when every lane's two codes take the one-put form, the four spread
+// lookups issued together and the two puts; otherwise the planes one at a
+// time (CUZFP_EXP_ENC2 A/B builds).
+template <int DIMS, typename PW, typename Writer>
+ZFP_HD void encode_plane_pair_step(PW xa, PW xb, unsigned& n, Writer& wr) {
+  const unsigned na = n;
+  const uint64_t ra = (uint64_t)xa >> na;
+  const uint32_t rla = (uint32_t)ra;
+  const uint32_t bla = bitlen16(rla);
+  const PlaneLen pa = plane_len<DIMS>(na, bla, (uint32_t)__builtin_popcount(rla) + bla);
+  const unsigned nb = pa.nn - pa.imp;
+  const uint64_t rb = (uint64_t)xb >> nb;
+  const uint32_t rlb = (uint32_t)rb;
+  const uint32_t blb = bitlen16(rlb);
+  const PlaneLen pb = plane_len<DIMS>(nb, blb, (uint32_t)__builtin_popcount(rlb) + blb);
+  const bool ok = ((ra | rb) >> 15) == 0 && pa.len <= 64u && pb.len <= 64u;
+  if (__builtin_expect(!any_lane(!ok), 1)) {
+    const uint32_t e0a = wr.sp0(byte_off4<0>(rla)), e1a = wr.sp1(byte_off4<1>(rla));
+    const uint32_t e0b = wr.sp0(byte_off4<0>(rlb)), e1b = wr.sp1(byte_off4<1>(rlb));
+    const uint32_t ga = low_bits((e0a >> 5) | (e1a << (e0a & 31u)), pa.width);
+    const uint32_t gb = low_bits((e0b >> 5) | (e1b << (e0b & 31u)), pb.width);
+    wr.put((uint64_t)xa ^ ((ra ^ (uint64_t)ga) << na), pa.len);
+    wr.put((uint64_t)xb ^ ((rb ^ (uint64_t)gb) << nb), pb.len);
+    n = pb.nn - pb.imp;
+  } else {
+    encode_plane_step<DIMS>(xa, n, wr);
+    encode_plane_step<DIMS>(xb, n, wr);
+  }
+}
+
+// Four 3D planes with one wave-uniform test (CUZFP_EXP_ENC4 A/B builds).
+template <int DIMS, typename PW, typename Writer>
+ZFP_HD void encode_plane_quad_step(PW x0, PW x1, PW x2, PW x3, unsigned& n, Writer& wr) {
+  const PW xs[4] = {x0, x1, x2, x3};
+  unsigned ns[4];
+  uint64_t rs[4];
+  PlaneLen ps[4];
+  unsigned m = n;
+  uint64_t any_hi = 0;
+  bool fit = true;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    ns[i] = m;
+    rs[i] = (uint64_t)xs[i] >> m;
+    const uint32_t rl = (uint32_t)rs[i];
+    const uint32_t bl = bitlen16(rl);
+    ps[i] = plane_len<DIMS>(m, bl, (uint32_t)__builtin_popcount(rl) + bl);
+    any_hi |= rs[i];
+    fit = fit && ps[i].len <= 64u;
+    m = ps[i].nn - ps[i].imp;
+  }
+  const bool ok = (any_hi >> 15) == 0 && fit;
+  if (__builtin_expect(!any_lane(!ok), 1)) {
+    uint32_t e0[4], e1[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      e0[i] = wr.sp0(byte_off4<0>((uint32_t)rs[i]));
+      e1[i] = wr.sp1(byte_off4<1>((uint32_t)rs[i]));
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const uint32_t gi = low_bits((e0[i] >> 5) | (e1[i] << (e0[i] & 31u)), ps[i].width);
+      wr.put((uint64_t)xs[i] ^ ((rs[i] ^ (uint64_t)gi) << ns[i]), ps[i].len);
+    }
+    n = m;
+  } else {
+    encode_plane_step<DIMS>(x0, n, wr);
+    encode_plane_step<DIMS>(x1, n, wr);
+    encode_plane_step<DIMS>(x2, n, wr);
+    encode_plane_step<DIMS>(x3, n, wr);
+  }
+}
+
 // Planes 31 .. cmin of 32-bit half H, two at a time (an odd one left at the
 // bottom goes alone); false once the block is full.
 template <int H, typename UInt, int DIMS, typename Writer>
@@ -874,8 +949,29 @@ ZFP_HD bool encode_half_fixed(const planes<UInt, DIMS>& P, unsigned& n, Writer& 
       else if constexpr (C == CUZFP_PRIO_T0) __builtin_amdgcn_s_setprio(0);
     }
 #endif
-    encode_plane_step<DIMS>((PW)P.template get<H>(C), n, wr);
-    encode_plane_step<DIMS>((PW)P.template get<H>(C - 1), n, wr);
+#if defined(CUZFP_EXP_ENC4)
+    if constexpr (DIMS == 3 && C % 4 == 3) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(CUZFP_NO_PRIO)
+      if constexpr (prio_of<Writer>::value && PRI) {  // the drops that fall inside these 4 planes
+        if constexpr (C >= CUZFP_PRIO_T0 && C - 4 < CUZFP_PRIO_T0) __builtin_amdgcn_s_setprio(0);
+        else if constexpr (C >= CUZFP_PRIO_T1 && C - 4 < CUZFP_PRIO_T1) __builtin_amdgcn_s_setprio(1);
+        else if constexpr (C >= CUZFP_PRIO_T2 && C - 4 < CUZFP_PRIO_T2) __builtin_amdgcn_s_setprio(2);
+      }
+#endif
+      encode_plane_quad_step<DIMS>((PW)P.template get<H>(C), (PW)P.template get<H>(C - 1),
+                                   (PW)P.template get<H>(C - 2), (PW)P.template get<H>(C - 3), n, wr);
+      return encode_half_fixed<H, C - 4, PRI>(P, n, wr);
+    }
+#endif
+#if defined(CUZFP_EXP_ENC2)
+    if constexpr (DIMS == 3) {
+      encode_plane_pair_step<DIMS>((PW)P.template get<H>(C), (PW)P.template get<H>(C - 1), n, wr);
+    } else
+#endif
+    {
+      encode_plane_step<DIMS>((PW)P.template get<H>(C), n, wr);
+      encode_plane_step<DIMS>((PW)P.template get<H>(C - 1), n, wr);
+    }
     return encode_half_fixed<H, C - 2, PRI>(P, n, wr);
   }
   return true;
