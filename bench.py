@@ -84,6 +84,11 @@ def parse():
     p.add_argument("--config5-edge", type=int, default=1024, help="edge of configs[4]'s global array")
     p.add_argument("--config5-steps", type=int, default=10)
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                   help="process-group backend for N > 1 (nccl = RCCL, the measured path; gloo runs the "
+                        "collectives on host copies: tests of the multi-rank bookkeeping)")
+    p.add_argument("--same-device", action="store_true",
+                   help="every rank on cuda:0 (tests of the N > 1 path on a one-GPU box; not a measurement)")
     p.add_argument("--dry-run-cpu", action="store_true",
                    help="test mode, no GPU: every rank runs the gloo backend and the CPU oracle stands in for "
                         "the codec, so the launcher and the rank bookkeeping can be checked on a CPU-only host; "
@@ -108,6 +113,40 @@ def launch_ranks(args) -> int:
     return subprocess.call(cmd, env=env)
 
 
+# Collectives of the bench's bookkeeping.  With RCCL they run on the device
+# tensors; with gloo (--backend gloo, tests of the N > 1 path) on host copies,
+# since gloo has no device collectives on this build.
+HOST_COLL = False
+
+
+def all_reduce_max(dist, t):
+    if HOST_COLL:
+        c = t.cpu()
+        dist.all_reduce(c, op=dist.ReduceOp.MAX)
+        t.copy_(c)
+    else:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+
+
+def all_gather_into(dist, out, t):
+    if HOST_COLL:
+        parts = list(torch_empty_like_cpu(out).chunk(dist.get_world_size()))
+        dist.all_gather(parts, t.cpu())
+        out.copy_(torch_cat(parts))
+    else:
+        dist.all_gather_into_tensor(out, t)
+
+
+def torch_empty_like_cpu(t):
+    import torch
+    return torch.empty(t.shape, dtype=t.dtype, device="cpu")
+
+
+def torch_cat(parts):
+    import torch
+    return torch.cat(parts)
+
+
 def rank_info(dist, world: int, dev, backend: str) -> dict:
     """What the ranks saw: the process group's size and backend, the devices
     this process can see, and every rank's device id (gathered)."""
@@ -117,7 +156,7 @@ def rank_info(dist, world: int, dev, backend: str) -> dict:
     if dist.is_initialized() and seen > 1:
         t = torch.tensor([did], dtype=torch.int64, device=dev)
         out = torch.empty(seen, dtype=torch.int64, device=dev)
-        dist.all_gather_into_tensor(out, t)
+        all_gather_into(dist, out, t)
         devs = [int(v) for v in out.cpu()]
     else:
         devs = [did]
@@ -233,6 +272,13 @@ def cpu_baseline(a: np.ndarray, maxbits: int):
             "wall_s": round(wall, 2)}
 
 
+def allgather_words(zd, words):
+    """The stream all-gather: RCCL on the device words, or gloo on a host copy."""
+    if HOST_COLL:
+        return zd.allgather_stream(words.cpu()).to(words.device)
+    return zd.allgather_stream(words)
+
+
 def run_config5(E: int, steps: int, world: int, rank: int, dev, graphed, dist):
     """BASELINE configs[4] at this N, GPU phase: one E^3 f32 polynomial
     array at rate 8 strong-scaled over the N ranks as z-slabs of E/N planes.  Each
@@ -263,7 +309,7 @@ def run_config5(E: int, steps: int, world: int, rank: int, dev, graphed, dist):
     def allmax(v: float) -> float:
         t = torch.tensor([v], dtype=torch.float64, device=dev)
         if world > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            all_reduce_max(dist, t)
         return float(t.item())
 
     def allgather_floats(v: float) -> list:
@@ -271,7 +317,7 @@ def run_config5(E: int, steps: int, world: int, rank: int, dev, graphed, dist):
         if world == 1:
             return [v]
         out = torch.empty(world, dtype=torch.float64, device=dev)
-        dist.all_gather_into_tensor(out, t)
+        all_gather_into(dist, out, t)
         return [float(u) for u in out.cpu()]
 
     per_graph = next(c for c in (5, 2, 1) if steps % c == 0)
@@ -308,21 +354,22 @@ def run_config5(E: int, steps: int, world: int, rank: int, dev, graphed, dist):
 
     ag_s, full = None, None
     if world > 1:
-        full = zd.allgather_stream(words)
+        full = allgather_words(zd, words)
         torch.cuda.synchronize()
         dist.barrier()
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         for _ in range(5):
-            full = zd.allgather_stream(words)
+            full = allgather_words(zd, words)
         e1.record(stream)
         torch.cuda.synchronize()
         dist.barrier()
         ag_s = allmax(e0.elapsed_time(e1) / 5 * 1e-3)
         if rank != 0:
             full = None
-    out = zd.sharded_summary(sh, 4, step_s, enc_s, dec_s, HBM_PEAK_GBS, ag_s)
+    out = zd.sharded_summary(sh, 4, step_s, enc_s, dec_s, HBM_PEAK_GBS, ag_s,
+                             "gloo (host-copy collectives)" if HOST_COLL else "nccl (RCCL)")
     out["steps"] = steps
     del x, y
     return {"record": out, "E": E, "words": words, "full": full, "err": err}
@@ -339,7 +386,7 @@ def finish_config5(st: dict, world: int, rank: int, dev, dist) -> dict:
     def allmax(v: float) -> float:
         t = torch.tensor([v], dtype=torch.float64, device=dev)
         if world > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            all_reduce_max(dist, t)
         return float(t.item())
 
     gold = None
@@ -380,11 +427,18 @@ def main():
     if world != args.gpus:  # a measurement of fewer ranks than asked for is never printed
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}: launch N ranks (python bench.py --gpus N "
                          f"starts them itself) or pass --gpus {world}")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    global HOST_COLL
+    gpu = 0 if args.same_device else local_rank
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    backend = "nccl (RCCL)" if args.backend == "nccl" else "gloo (host-copy collectives)"
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+            HOST_COLL = True
 
     dtype = np.dtype(args.dtype)
     n = args.size
@@ -522,21 +576,21 @@ def main():
     # optional RCCL all-gather of the compressed stream (the exchange step)
     allgather = None
     if world > 1 and zd.uniform_shard_ok(gshape, world, maxbits):
-        full = zd.allgather_stream(words)
+        full = allgather_words(zd, words)
         torch.cuda.synchronize()
         dist.barrier()
         ag0 = time.perf_counter()
         agr = 5
         for _ in range(agr):
-            full = zd.allgather_stream(words)
+            full = allgather_words(zd, words)
         torch.cuda.synchronize()
         ag_s = (time.perf_counter() - ag0) / agr
         t = torch.tensor([ag_s], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        all_reduce_max(dist, t)
         ag_s = float(t.item())
         allgather = {"bytes_per_rank_in": int(full.numel() * 8 - nbytes_stream), "ms": round(ag_s * 1e3, 3),
                      "GBps_per_rank_in": round((full.numel() * 8 - nbytes_stream) / ag_s / 1e9, 2),
-                     "backend": "nccl (RCCL)"}
+                     "backend": backend}
         del full
 
     # (last before the warmup steps: the ~100 ms of back-to-back kernels bring
@@ -576,7 +630,7 @@ def main():
     wall = time.perf_counter() - t0
     t_local = torch.tensor([wall], dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(t_local, op=dist.ReduceOp.MAX)
+        all_reduce_max(dist, t_local)
     elapsed = float(t_local.item())
     gpu_ms_per_step = ev0.elapsed_time(ev1) / args.steps
 
@@ -615,7 +669,7 @@ def main():
         except Exception:
             traffic = None
 
-    ranks = rank_info(dist, world, dev, "nccl (RCCL)" if world > 1 else "none")
+    ranks = rank_info(dist, world, dev, backend if world > 1 else "none")
     result = None
     if rank == 0:
         host_path = None

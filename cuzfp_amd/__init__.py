@@ -176,13 +176,18 @@ def encode(x, maxbits: int, out=None, stream=None):
     if _broadcast(x):
         # materialise a broadcast view (a zero stride means "contiguous" to the
         # C-ABI) on the launch stream, after the work already queued on torch's
-        # current stream, and keep the copy alive until the kernel that reads
-        # it has run (record_stream: the caching allocator waits for that stream)
-        s = torch.cuda.current_stream(x.device) if stream is None else stream
-        s.wait_stream(torch.cuda.current_stream(x.device))
+        # current stream.  The copy is allocated on that stream, so the kernel
+        # that reads it is ordered before any reuse; the broadcast source was
+        # allocated on the current stream and is read on s, so it is recorded
+        # there (the caching allocator then waits for s before reusing it).
+        cur = torch.cuda.current_stream(x.device)
+        s = cur if stream is None else stream
+        s.wait_stream(cur)
+        src = x
         with torch.cuda.stream(s):
-            x = x.contiguous()
-        x.record_stream(s)
+            x = src.contiguous()
+        if s != cur:
+            src.record_stream(s)
     t = type_code(x.dtype)
     nx, ny, nz = _extents(x.shape)
     nbytes = stream_bytes(x.shape, x.dtype, maxbits)

@@ -1099,6 +1099,13 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) voi
 // runtime cannot say.  Thread-safe: each device's slot is an atomic written
 // with the same value by whichever thread reads it first.
 static inline size_t lds_cap_bytes() {
+  // CUZFP_LDS_CAP_BYTES (read once a process) lowers the budget, so that the
+  // launchers' refusal of a block image that cannot fit is testable on gfx950
+  static const long forced = [] {
+    const char* e = getenv("CUZFP_LDS_CAP_BYTES");
+    return (e && *e) ? atol(e) : 0L;
+  }();
+  if (forced > 0) return (size_t)forced;
   static std::atomic<int> cap[kMaxDevices];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return 65536;
@@ -1210,6 +1217,8 @@ int launch_encode_t(const void* data, const Geometry& g, bool fast, uint64_t* st
   // (whose padded image would pass the workgroup's LDS) take the general writer
   const bool aligned = (g.maxbits & 63) == 0 && gg.lds_words * 8 + kStatic <= lds_cap_bytes();
   if (!aligned) gg.lds_words = g.maxbits + 2;
+  // one wave's image beside the tables must fit the workgroup's LDS budget
+  if (gg.lds_words * 8 + kStatic > lds_cap_bytes()) return CUZFP_ERROR_INVALID_ARGUMENT;
   const uint32_t wpg = waves_per_group(gg.lds_words, kStatic, kEncWaves);
   const dim3 grid((nwaves + wpg - 1) / wpg), block(kLanes * wpg);
   const size_t lds = (size_t)wpg * gg.lds_words * 8;
@@ -1246,7 +1255,10 @@ int launch_decode_t(const uint64_t* stream, const Geometry& g, bool fast, void* 
   // blocks of at most 64 bits are read into registers (RegReader): no LDS image
   const bool reg = DIMS <= 2 && g.maxbits <= 64;
   if (reg) gg.lds_words = 0;
-  const uint32_t wpg = waves_per_group(gg.lds_words, kChunkLutBytes + (DIMS == 1 ? sizeof(Plane1dDecLut) : 16), kDecWaves);
+  const size_t kStatic = kChunkLutBytes + (DIMS == 1 ? sizeof(Plane1dDecLut) : 16);
+  // one wave's image beside the tables must fit the workgroup's LDS budget
+  if (gg.lds_words * 8 + kStatic > lds_cap_bytes()) return CUZFP_ERROR_INVALID_ARGUMENT;
+  const uint32_t wpg = waves_per_group(gg.lds_words, kStatic, kDecWaves);
   const dim3 grid((nwaves + wpg - 1) / wpg), block(kLanes * wpg);
   const size_t lds = (size_t)wpg * gg.lds_words * 8;  // (+ the static chunk tables)
   Scalar* d = (Scalar*)data;

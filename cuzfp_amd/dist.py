@@ -99,7 +99,8 @@ class StrongShard:
 
 
 def sharded_summary(shard: "StrongShard", itemsize: int, step_s: float, enc_s: list, dec_s: list,
-                    hbm_peak_GBps: float, allgather_s: float | None = None) -> dict:
+                    hbm_peak_GBps: float, allgather_s: float | None = None,
+                    backend: str = "nccl (RCCL)") -> dict:
     """The bench line's record of one strong-scaled sharded run: `step_s` is the
     max over ranks of one encode+decode step, enc_s / dec_s the per-rank kernel
     times (seconds), allgather_s the max-over-ranks all-gather time."""
@@ -118,7 +119,7 @@ def sharded_summary(shard: "StrongShard", itemsize: int, step_s: float, enc_s: l
         recv = stream - shard.words * 8               # bytes each rank receives
         out["allgather"] = {"ms": round(allgather_s * 1e3, 4), "bytes_in_per_rank": recv,
                             "GBps_in_per_rank": round(recv / allgather_s / 1e9, 2) if allgather_s > 0 else None,
-                            "backend": "nccl (RCCL)"}
+                            "backend": backend}
     return out
 
 

@@ -12,7 +12,9 @@
 // Differences, all in the direction of CPU zfp 0.5.0 (the reference's own
 // oracle, src/utils/test.py:68-93): non-zero field strides are honoured; any
 // maxbits in [1 + exponent bits, CUZFP_MAX_BITS = 16384] works in every
-// dimensionality (zfp's ZFP_MAX_BITS, the most bits a block can use, is 4171);
+// dimensionality on gfx950 (zfp's ZFP_MAX_BITS, the most bits a block can use,
+// is 4171; on a device with less LDS a block image that does not fit fails
+// with CUZFP_ERROR_INVALID_ARGUMENT, include/cuzfp_hip.h);
 // partial blocks are padded as CPU zfp pads them; failures print one line to
 // stderr and compress returns 0 (the reference prints and continues).
 // One addition: cuZFP_last_status() returns the status code (include/cuzfp_hip.h)

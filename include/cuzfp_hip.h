@@ -62,8 +62,11 @@ extern "C" {
  * padding.  The bound keeps one wave's LDS stream image within a gfx950
  * workgroup's LDS (160 KiB, hipDeviceAttributeMaxSharedMemoryPerBlock): the
  * decoder's image at 16384 bits is 129 KiB plus 12 KiB of tables.  On a device
- * with less LDS per workgroup a call whose image does not fit returns
- * CUZFP_ERROR_INVALID_ARGUMENT. */
+ * with less LDS per workgroup (e.g. 64 KiB) the launchers check one wave's image
+ * plus the tables against the device's budget before launching and return
+ * CUZFP_ERROR_INVALID_ARGUMENT for a call that does not fit (3D f32/f64 past
+ * about 6,500 bits on a 64 KiB device); the environment variable
+ * CUZFP_LDS_CAP_BYTES lowers the budget (tests). */
 #define CUZFP_MAX_BITS 16384
 
 /* Streams the host-memory pipeline is measured best with (callers' default

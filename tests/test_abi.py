@@ -131,6 +131,32 @@ def test_maxbits_cap(libs):
     assert lib.cuzfp_hip_maximum_size(3, 16, 16, 16, cap + 1) == 0
 
 
+def test_lds_budget_refusal(libs):
+    """On a device with less LDS a workgroup (CUZFP_LDS_CAP_BYTES forces 64 KiB,
+    read once a process) a block image that cannot fit beside the tables is
+    refused with CUZFP_ERROR_INVALID_ARGUMENT before any launch (the
+    launchers used to go ahead with one wave a workgroup and fail as a HIP
+    error).  Fake pointers: the refusal comes before anything touches them."""
+    code = r"""
+import ctypes, sys
+sys.path.insert(0, %r)
+import cuzfp_amd as cz
+lib = cz.library()
+got = ctypes.c_size_t(0)
+buf = ctypes.c_void_p(0x1000)
+out = []
+for t, dims in ((3, (16, 16, 16)), (4, (16, 16, 16)), (3, (64, 64, 0)), (3, (256, 0, 0))):
+    nx, ny, nz = dims
+    out.append(lib.cuzfp_hip_encode(buf, t, nx, ny, nz, 0, 0, 0, 16384, buf, 1 << 30, ctypes.byref(got), None))
+    out.append(lib.cuzfp_hip_decode(buf, 1 << 30, t, nx, ny, nz, 0, 0, 0, 16384, buf, None))
+print(out)
+""" % ROOT
+    env = dict(os.environ, CUZFP_LDS_CAP_BYTES="65536")
+    r = subprocess.run([os.sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip() == str([1] * 8), r.stdout
+
+
 def test_host_out_checks(libs):
     """compress_host / decompress_host validate a caller's `out` before the
     C side writes through it (contiguity, dtype, shape, size)."""

@@ -7,6 +7,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -44,3 +46,30 @@ def test_single_rank_dry_run():
     assert r.returncode == 0, r.stderr[-2000:]
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
     assert d["n_gpus"] == 1 and d["world_size_seen"] == 1
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(290)
+def test_gpus2_gloo_same_device_bench():
+    """bench.main()'s N > 1 path on a one-GPU box (verdict r03): two ranks on
+    cuda:0, gloo with host-copy collectives in place of RCCL.  Exercises the
+    multi-rank bookkeeping the driver's scaling run depends on -- the rank
+    gather, max-over-ranks timing, configs[4] strong-scaled over 2 z-slabs with
+    its all-gather and the per-slab reference hashes -- before such a run does.
+    Not a measurement (two ranks share one GPU)."""
+    r = _run(["--gpus", "2", "--backend", "gloo", "--same-device", "--steps", "10", "--warmup", "2",
+              "--no-cpu-baseline", "--no-host-path", "--no-copy-probe", "--config5-steps", "2",
+              "--kernel-ms", "5"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["world_size_seen"] == 2
+    assert d["rank_devices"] == [0, 0]
+    assert d["backend"].startswith("gloo")
+    c5 = d["config5"]
+    assert c5["n_ranks"] == 2 and len(c5["encode_ms_per_rank"]) == 2
+    assert c5["parity"]["slabs_match_reference_word_ranges"] is True
+    assert c5["parity"]["stream_matches_reference"] is True
+    assert c5["allgather"]["backend"].startswith("gloo")
+    assert d["allgather"] is not None and d["value"] > 0

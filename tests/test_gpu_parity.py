@@ -361,6 +361,28 @@ def test_register_reader(cuda, restatement, dims, dtype):
             assert np.array_equal(y.view(np.uint8), restatement.decompress(ref, shape, dtype, mb).view(np.uint8)), mb
 
 
+@pytest.mark.parametrize("mb", [32, 64])
+@pytest.mark.parametrize("dims", [1, 2])
+@pytest.mark.parametrize("dtype", [np.int32, np.int64])
+def test_int_register_writer(cuda, restatement, dims, dtype, mb):
+    """Integer blocks of 32 and 64 bits (1D / 2D): the register writer
+    (RegWriter, FULL64 masking at 64) and register reader, against the
+    restatement's block-level int32 / int64 coder; 1D at more than 32,768 waves
+    as well (integer fields take the general-gather kernels at every size)."""
+    rng = np.random.default_rng(mb + 10 * dims + np.dtype(dtype).itemsize)
+    shapes = [(4 * 64 * 5 + 9,), (4 * 64 * 32769 + 6,)] if dims == 1 else [(90, 75), (1030, 517)]
+    for shape in shapes:
+        for kind in ("uniform", "smooth"):
+            if kind == "uniform":
+                a = rng.integers(-2 ** 24, 2 ** 24, size=shape).astype(dtype)
+            else:
+                a = np.cumsum(rng.integers(-1000, 1000, size=shape), axis=-1).astype(dtype)
+            words, y = _gpu_roundtrip(a, mb, cuda)
+            ref = restatement.compress(a, mb)
+            assert np.array_equal(words, ref), (shape, kind)
+            assert np.array_equal(y, restatement.decompress(ref, shape, dtype, mb)), (shape, kind)
+
+
 @pytest.mark.parametrize("nblocks", [64 * 32771, 64 * 32769 + 25, 64 * 32768 - 1])
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 def test_batched_1d_waves(cuda, restatement, nblocks, dtype):
@@ -439,7 +461,10 @@ def test_host_cache_release(cuda, restatement):
 def test_broadcast_view_side_stream(cuda, restatement):
     """A broadcast view encoded on a side stream: the materialising copy runs on
     that stream after the current stream's pending work (here the kernel that
-    writes the base tensor) and stays allocated until the encode has read it."""
+    writes the base tensor), and the base stays allocated until that copy has
+    read it (record_stream on the side stream).  The side stream is held back by
+    a spin kernel, so without the record a same-size allocation on the current
+    stream reuses the freed base and overwrites it with NaNs before the copy."""
     import torch
     side = torch.cuda.Stream(device=cuda)
     mb = cz.rate_to_maxbits(8, np.float32, 3)
@@ -447,11 +472,15 @@ def test_broadcast_view_side_stream(cuda, restatement):
         base = torch.empty(64, dtype=torch.float32, device=cuda)
         # exact values (power-of-two scale), written by a kernel queued on the current stream
         base.copy_(torch.arange(64, dtype=torch.float32, device=cuda) * (trial + 1) / 64 - 0.5)
+        with torch.cuda.stream(side):
+            torch.cuda._sleep(20_000_000)  # the side stream's copy runs well after the lines below
         x = base.expand(40, 32, 64)
         w = cz.encode(x, mb, stream=side)
         del x, base
-        junk = torch.full((40 * 32 * 64,), float("nan"), device=cuda)  # would reuse a freed copy's memory
+        junk = torch.empty(64, dtype=torch.float32, device=cuda)  # base's size class, current stream
+        junk.fill_(float("nan"))
         side.synchronize()
+        torch.cuda.synchronize()
         vals = np.arange(64, dtype=np.float32) * np.float32(trial + 1) / np.float32(64) - np.float32(0.5)
         ref = restatement.compress(np.broadcast_to(vals, (40, 32, 64)).copy(), mb)
         assert np.array_equal(w.cpu().numpy().view(np.uint64), ref), trial
