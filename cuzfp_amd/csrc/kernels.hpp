@@ -75,11 +75,7 @@ __device__ const Pair1dLut g_pair1d_lut = make_pair1d_lut();
 __device__ const Plane1dDecLut g_plane1d_lut = make_plane1d_dec_lut();
 constexpr size_t kSpreadTabBytes = sizeof(SpreadTab);
 typedef __attribute__((address_space(3))) const uint32_t lds_spread;
-#if !defined(CUZFP_EXP_P1D_NOLDS)
 typedef lds_spread* P1dPtr;
-#else
-typedef const uint32_t* P1dPtr;
-#endif
 
 // ---------------------------------------------------------------------------
 // LDS bit writers / reader (one lane, one block)
@@ -101,9 +97,6 @@ struct LdsOrWriter {
   uint32_t pos, lim;    // bits produced; 64 * W
   P1dPtr p1d;           // 1D: the workgroup's pair table (Pair1dLut)
   __device__ __forceinline__ uint32_t pair1d(uint32_t o) const { return *(P1dPtr)((uintptr_t)p1d + o); }
-#if defined(CUZFP_EXP_NOPUT)
-  uint64_t sink = 0;
-#endif
   __device__ __forceinline__ bool full() const { return pos >= lim; }
   __device__ __forceinline__ void put(uint64_t v, unsigned n) {  // v < 2^n
     const uint32_t w = pos >> 6;
@@ -123,11 +116,7 @@ struct LdsOrWriter {
   __device__ __forceinline__ uint32_t sp1(uint32_t o) const { return *(lds_spread*)((uintptr_t)(lut + 256) + o); }
   __device__ __forceinline__ uint32_t spread(uint32_t b) const { return lut[256 + b] >> 1; }
   __device__ __forceinline__ void zero_bit() { pos++; }
-#if defined(CUZFP_EXP_NOPUT)
-  __device__ __forceinline__ void finish() { p[0] ^= sink; }
-#else
   __device__ __forceinline__ void finish() {}
-#endif
   // a full lane keeps stepping with its wave: restart it at the first slack
   // row each plane, so its (discarded) pieces stay within rows W .. W + 3
   __device__ __forceinline__ void settle() { pos = pos < lim ? pos : lim; }
@@ -145,9 +134,6 @@ struct LdsBitWriter {
   uint64_t acc;
   P1dPtr p1d;              // 1D: the workgroup's pair table (Pair1dLut)
   __device__ __forceinline__ uint32_t pair1d(uint32_t o) const { return *(P1dPtr)((uintptr_t)p1d + o); }
-#if defined(CUZFP_EXP_NOPUT)
-  uint64_t sink = 0;
-#endif
   __device__ __forceinline__ uint32_t sp0(uint32_t o) const { return *(lds_spread*)((uintptr_t)lut + o); }
   __device__ __forceinline__ uint32_t sp1(uint32_t o) const { return *(lds_spread*)((uintptr_t)(lut + 256) + o); }
   __device__ __forceinline__ uint32_t spread(uint32_t b) const { return lut[256 + b] >> 1; }
@@ -244,11 +230,6 @@ struct LdsReader {
   }
   // table decoder: 64 bits at pos and 32 bits at pos + m, read fresh
   __device__ __forceinline__ void windows(uint32_t m, uint64_t& w, uint32_t& g) const {
-#if defined(CUZFP_EXP_DEC_NOWIN)  // timing experiment (tools/variants.py): no window reads, wrong output
-    w = (uint64_t)(pos * 0x9e3779b9u) * 0x100000001ull;
-    g = (pos + m) * 0x85ebca6bu;
-    return;
-#endif
     const uint32_t q = pos + m;
     lds_u32* r = row(pos);
     lds_u32* t = row(q);
@@ -266,11 +247,7 @@ struct LdsReader {
   // so the offsets are built with the fewest instructions, three-input ones
   // included.)
   __device__ __forceinline__ uint32_t tab(uint32_t byte_off) const {
-#if defined(CUZFP_EXP_GTAB)  // timing experiment: the tables read through the vector L1 instead of LDS
-    return *(const uint32_t*)((const char*)g_chunk_lut.e + byte_off);
-#else
     return *(lds_u32*)((uintptr_t)(lds_u32*)lut32 + byte_off);
-#endif
   }
   // g with every bit cleared unless its leading group test (bit 0) is 1: a
   // lane whose test reads "0" (no new ones: about half the lane-steps) looks
@@ -279,9 +256,6 @@ struct LdsReader {
   // instead of bank conflicts (random entries made 51 % of the decoder's LDS
   // cycles conflict cycles, SQ_LDS_BANK_CONFLICT)
   static __device__ __forceinline__ uint32_t lead_masked(uint32_t g) {
-#if defined(CUZFP_EXP_NOLEAD)  // A/B: unmasked (more bank conflicts, two VALU fewer)
-    return g;
-#endif
     uint32_t t;
     asm("v_bfe_i32 %0, %1, 0, 1" : "=v"(t) : "v"(g));
     return g & t;
@@ -302,11 +276,7 @@ struct LdsReader {
   static constexpr uint32_t kPairBytes = 4u * kLutPairs;  // byte address of the pair table
   typedef __attribute__((address_space(3))) const uint64_t lds_u64;
   __device__ __forceinline__ uint2 tab64(uint32_t byte_off) const {
-#if defined(CUZFP_EXP_GTAB)
-    const uint64_t v = *(const uint64_t*)((const char*)g_chunk_lut.e + byte_off);
-#else
     const uint64_t v = *(lds_u64*)((uintptr_t)(lds_u32*)lut32 + byte_off);
-#endif
     return uint2{(uint32_t)v, (uint32_t)(v >> 32)};
   }
   // the table steps' lookups: entry (2, g's chunk 1) and the pair (0, chunk 2),
@@ -314,11 +284,6 @@ struct LdsReader {
   // position's bit alone; the parse then runs past position N-1, which the
   // steps' implied-one rule resolves.)
   __device__ __forceinline__ void chunks_fast(uint32_t g, uint32_t& e1, uint32_t& e2a, uint32_t& e2b) const {
-#if defined(CUZFP_EXP_DEC_NOLUT)  // timing experiment: no table reads (short ended codes), wrong output
-    e1 = pack_entry(g & 0x3ffu, ((g >> 10) & 7u) + 1u, ((g >> 13) & 7u) + 1u, 0);
-    e2a = e2b = 0;
-    return;
-#endif
     const uint32_t gm = lead_masked(g);
     e1 = tab(off1(gm));
     const uint2 p = tab64(kPairBytes + off2(gm));
@@ -679,17 +644,11 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS, true>::value
     // ... and the 64 bytes of spread table 1D reads (entries 0-15 of table 0:
     // r = x >> n < 2^4), behind the same barrier
     if (threadIdx.x < 4) ((uint4*)stab)[threadIdx.x] = ((const uint4*)g_spread_tab.e)[threadIdx.x];
-#if !defined(CUZFP_EXP_P1D_NOLDS)
     for (uint32_t i = threadIdx.x; i < sizeof(Pair1dLut) / 16; i += blockDim.x)
       ((uint4*)ptab)[i] = ((const uint4*)g_pair1d_lut.e)[i];
-#endif
     __syncthreads();
   }
-#if !defined(CUZFP_EXP_P1D_NOLDS)
   lds_spread* p1d = (lds_spread*)ptab;
-#else  // timing experiment: the pair table read through the vector caches, no LDS copy
-  const uint32_t* p1d = g_pair1d_lut.e;
-#endif
   if (!live_wave) return;
   // the plane coder's spread tables, written whole by every wave (see
   // g_spread_tab): their load is issued first so that storing them waits only
@@ -715,41 +674,12 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS, true>::value
   // W words per block plus kSlackWords rows
   const uint32_t W = g.maxbits >> 6;
   Scalar f[N];
-#if defined(CUZFP_EXP_NOLOAD)  // timing experiment (tools/variants.py): a synthetic smooth block, no HBM reads
-  for (int i = 0; i < N; i++) f[i] = (Scalar)(1.0f + 0.001f * (float)((b & 255) + 3 * i + (i >> 2) * (i & 3)));
-#elif defined(CUZFP_EXP_GENLOAD)  // timing experiment (tools/xvar.py): the bench's polynomial field computed
-  // in the kernel with the generator's IEEE operations (cuzfp_amd/datagen.py), so the
-  // block's values -- and the stream -- are the bench's, without HBM reads
-  if (b < g.nblocks) {
-    const BlockPos bp = block_pos<DIMS>(g, b);
-    auto axis = [](uint32_t i, uint32_t n) {
-      const float x = __fdiv_rn((float)(int)(2 * i - n + 1), (float)n);
-      const float xx = __fmul_rn(x, x);
-      const float yy = __fsub_rn(__fmul_rn(xx, 4.0f), 3.0f);
-      return __fadd_rn(x, __fmul_rn(xx, yy));
-    };
-    for (int z = 0; z < 4; z++)
-      for (int y = 0; y < 4; y++)
-        for (int x = 0; x < 4; x++)
-          f[16 * z + 4 * y + x] = (Scalar)__fmul_rn(__fmul_rn(axis(4 * bp.ix + x, g.nx), axis(4 * bp.iy + y, g.ny)),
-                                                    axis(4 * bp.iz + z, g.nz));
-#if defined(CUZFP_EXP_GENBOTH)  // ... and the real gathers too, each value + 0 * its loaded twin
-    Scalar h[N];
-    gather<Scalar, DIMS, FAST>(data, g, bp, h);
-    for (int i = 0; i < N; i++) f[i] = f[i] + h[i] * (Scalar)0;
-#endif
-  }
-#else
   if (b < g.nblocks) gather<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
-#endif
   // (one copy a workgroup behind a barrier measured slower: 28.0 -> 28.4 us at 256^3)
   if constexpr (!kGroupSpread) {
 #pragma unroll
     for (uint32_t i = 0; i < kTabPieces / kLanes; i++) ((uint4*)stab)[lane + i * kLanes] = tab16[i];
   }
-#if defined(CUZFP_EXP_PAD) && defined(__HIP_DEVICE_COMPILE__) && CUZFP_EXP_PAD_AT == 0
-  exp_pad(lane);  // timing experiment: dummy VALU work while the gathers are in flight
-#endif
   if constexpr (REG) {
     wave_lds_sync();  // the spread tables
     uint64_t bits = 0;
@@ -863,10 +793,8 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) voi
       blk = ((uint64_t)__builtin_amdgcn_alignbit(a1, a0, s0) |
              ((uint64_t)__builtin_amdgcn_alignbit(a2, a1, s0) << 32)) & lowmask(g.maxbits);
     }
-#if !defined(CUZFP_EXP_GTAB)
     for (uint32_t i = threadIdx.x; i < kLutEnd; i += blockDim.x)
       ((uint4*)lut)[i] = ((const uint4*)g_chunk_lut.e)[i];
-#endif
     copy_dtab();
   } else {
     const uint32_t D = (g.maxbits + 31) >> 5;  // dwords per block
@@ -948,15 +876,7 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) voi
     }
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);  // a wave out of the coder stores at once
     if (coded) {
-#if defined(CUZFP_EXP_NOSTORE)  // timing experiment: one value a block reaches HBM
-      {
-        Scalar acc = f[0];
-        for (int i = 1; i < N; i++) acc += f[i];
-        if (acc == (Scalar)1234.5678) data[b] = acc;
-      }
-#else
       scatter<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
-#endif
     } else {  // a zero block
       Scalar z[N];
 #pragma unroll
@@ -1157,10 +1077,10 @@ static inline bool use_priority(uint32_t nwaves, int waves_per_simd, uint32_t ro
   return nwaves <= (uint32_t)c * 4u * (uint32_t)waves_per_simd * rounds;
 }
 
-#if defined(CUZFP_EXP_NOREG)  // A/B builds: no register-writer encoder
-constexpr bool kExpNoReg = true;
+#if defined(CUZFP_XVAR)  // tools/xvar.py builds: the fast-gather kernels only (compile time)
+constexpr bool kFastOnly = true;
 #else
-constexpr bool kExpNoReg = false;
+constexpr bool kFastOnly = false;
 #endif
 #ifndef CUZFP_ENC_PRIO_ROUNDS  // A/B builds: 0 = the encoder never takes the schedule
 #define CUZFP_ENC_PRIO_ROUNDS 1
@@ -1176,7 +1096,7 @@ int launch_encode_t(const void* data, const Geometry& g, bool fast, uint64_t* st
   // the kernel's static LDS: the spread tables, and in 1D the pair table
   constexpr size_t kStatic = kSpreadTabBytes + (DIMS == 1 ? sizeof(Pair1dLut) : 16);
   const Scalar* d = (const Scalar*)data;
-  if constexpr (DIMS <= 2 && !kExpNoReg) {
+  if constexpr (DIMS <= 2) {
     // maxbits 32 or 64: the register writer, blocks stored straight from it
     if (g.maxbits == 32 || g.maxbits == 64) {
       gg.lds_words = 0;
@@ -1226,19 +1146,14 @@ int launch_encode_t(const void* data, const Geometry& g, bool fast, uint64_t* st
     hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, true, true, false>), grid, block, lds, st, d, gg, stream);
   else if (fast && aligned)
     hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, true, true>), grid, block, lds, st, d, gg, stream);
-#if defined(CUZFP_EXP_ONLY3D)
   else if (fast)
     hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, true, false>), grid, block, lds, st, d, gg, stream);
-  else
+  else if constexpr (kFastOnly)
     return CUZFP_ERROR_UNSUPPORTED_TYPE;
-#else
-  else if (fast)
-    hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, true, false>), grid, block, lds, st, d, gg, stream);
   else if (aligned)
     hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, false, true>), grid, block, lds, st, d, gg, stream);
   else
     hipLaunchKernelGGL((zfp_encode<Scalar, DIMS, false, false>), grid, block, lds, st, d, gg, stream);
-#endif
   const hipError_t e = hipGetLastError();
   t_last_hip = e;
   return e == hipSuccess ? CUZFP_SUCCESS : CUZFP_ERROR_HIP;
@@ -1298,44 +1213,19 @@ int launch_decode_t(const uint64_t* stream, const Geometry& g, bool fast, void* 
     hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, true, false>), grid, block, lds, st, stream, gg, d);
   else if (fast)
     hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, true>), grid, block, lds, st, stream, gg, d);
-#if !defined(CUZFP_EXP_ONLY3D)
-  else
+  else if constexpr (!kFastOnly)
     hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, false>), grid, block, lds, st, stream, gg, d);
-#endif
   const hipError_t e = hipGetLastError();
   t_last_hip = e;
   return e == hipSuccess ? CUZFP_SUCCESS : CUZFP_ERROR_HIP;
 }
 
 
-// Per-type entry points (declared in launch.hpp).  Experiment builds
-// (tools/xvar.py, never the product library): CUZFP_EXP_ONLY3D instantiates
-// the 3D fast-gather kernels alone, CUZFP_EXP_STUB no kernel at all, so that
-// a timing variant of the 3D f32 kernels compiles in a fraction of the time.
-#if defined(CUZFP_EXP_ONLY3D) || defined(CUZFP_EXP_STUB)
-template <typename Scalar>
-int launch_encode_type(const Problem& p, const void* data, bool fast, uint64_t* stream,
-                       uint32_t wave0, uint32_t nwaves, hipStream_t st) {
-#if defined(CUZFP_EXP_ONLY3D)
-#ifndef CUZFP_EXP_DIMS
-#define CUZFP_EXP_DIMS 3
-#endif
-  if (p.dims == CUZFP_EXP_DIMS && fast)
-    return launch_encode_t<Scalar, CUZFP_EXP_DIMS>(data, p.g, fast, stream, wave0, nwaves, st);
-#endif
-  (void)p, (void)data, (void)fast, (void)stream, (void)wave0, (void)nwaves, (void)st;
-  return CUZFP_ERROR_UNSUPPORTED_TYPE;
-}
-template <typename Scalar>
-int launch_decode_type(const Problem& p, const uint64_t* stream, bool fast, void* data,
-                       uint32_t wave0, uint32_t nwaves, hipStream_t st) {
-#if defined(CUZFP_EXP_ONLY3D)
-  if (p.dims == CUZFP_EXP_DIMS && fast)
-    return launch_decode_t<Scalar, CUZFP_EXP_DIMS>(stream, p.g, fast, data, wave0, nwaves, st);
-#endif
-  (void)p, (void)data, (void)fast, (void)stream, (void)wave0, (void)nwaves, (void)st;
-  return CUZFP_ERROR_UNSUPPORTED_TYPE;
-}
+// Per-type entry points (declared in launch.hpp).  tools/xvar.py's timing
+// variants (never the product library) build the 3D fast-gather kernels alone
+// from tools/xvar_launch.hpp instead.
+#if defined(CUZFP_XVAR)
+#include "../../tools/xvar_launch.hpp"
 #else
 template <typename Scalar>
 int launch_encode_type(const Problem& p, const void* data, bool fast, uint64_t* stream,

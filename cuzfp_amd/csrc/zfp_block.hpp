@@ -831,81 +831,6 @@ ZFP_HD void encode_plane_step(PW x, unsigned& n, Writer& wr) {
   }
 }
 
-// Two 3D planes with one wave-uniform test: both planes' lengths first (the
-// second plane's n follows from the first's bit length alone, no table read),
-// then, when every lane's two codes take the one-put form, the four spread
-// lookups issued together and the two puts; otherwise the planes one at a
-// time (CUZFP_EXP_ENC2 A/B builds).
-template <int DIMS, typename PW, typename Writer>
-ZFP_HD void encode_plane_pair_step(PW xa, PW xb, unsigned& n, Writer& wr) {
-  const unsigned na = n;
-  const uint64_t ra = (uint64_t)xa >> na;
-  const uint32_t rla = (uint32_t)ra;
-  const uint32_t bla = bitlen16(rla);
-  const PlaneLen pa = plane_len<DIMS>(na, bla, (uint32_t)__builtin_popcount(rla) + bla);
-  const unsigned nb = pa.nn - pa.imp;
-  const uint64_t rb = (uint64_t)xb >> nb;
-  const uint32_t rlb = (uint32_t)rb;
-  const uint32_t blb = bitlen16(rlb);
-  const PlaneLen pb = plane_len<DIMS>(nb, blb, (uint32_t)__builtin_popcount(rlb) + blb);
-  const bool ok = ((ra | rb) >> 15) == 0 && pa.len <= 64u && pb.len <= 64u;
-  if (__builtin_expect(!any_lane(!ok), 1)) {
-    const uint32_t e0a = wr.sp0(byte_off4<0>(rla)), e1a = wr.sp1(byte_off4<1>(rla));
-    const uint32_t e0b = wr.sp0(byte_off4<0>(rlb)), e1b = wr.sp1(byte_off4<1>(rlb));
-    const uint32_t ga = low_bits((e0a >> 5) | (e1a << (e0a & 31u)), pa.width);
-    const uint32_t gb = low_bits((e0b >> 5) | (e1b << (e0b & 31u)), pb.width);
-    wr.put((uint64_t)xa ^ ((ra ^ (uint64_t)ga) << na), pa.len);
-    wr.put((uint64_t)xb ^ ((rb ^ (uint64_t)gb) << nb), pb.len);
-    n = pb.nn - pb.imp;
-  } else {
-    encode_plane_step<DIMS>(xa, n, wr);
-    encode_plane_step<DIMS>(xb, n, wr);
-  }
-}
-
-// Four 3D planes with one wave-uniform test (CUZFP_EXP_ENC4 A/B builds).
-template <int DIMS, typename PW, typename Writer>
-ZFP_HD void encode_plane_quad_step(PW x0, PW x1, PW x2, PW x3, unsigned& n, Writer& wr) {
-  const PW xs[4] = {x0, x1, x2, x3};
-  unsigned ns[4];
-  uint64_t rs[4];
-  PlaneLen ps[4];
-  unsigned m = n;
-  uint64_t any_hi = 0;
-  bool fit = true;
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    ns[i] = m;
-    rs[i] = (uint64_t)xs[i] >> m;
-    const uint32_t rl = (uint32_t)rs[i];
-    const uint32_t bl = bitlen16(rl);
-    ps[i] = plane_len<DIMS>(m, bl, (uint32_t)__builtin_popcount(rl) + bl);
-    any_hi |= rs[i];
-    fit = fit && ps[i].len <= 64u;
-    m = ps[i].nn - ps[i].imp;
-  }
-  const bool ok = (any_hi >> 15) == 0 && fit;
-  if (__builtin_expect(!any_lane(!ok), 1)) {
-    uint32_t e0[4], e1[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      e0[i] = wr.sp0(byte_off4<0>((uint32_t)rs[i]));
-      e1[i] = wr.sp1(byte_off4<1>((uint32_t)rs[i]));
-    }
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const uint32_t gi = low_bits((e0[i] >> 5) | (e1[i] << (e0[i] & 31u)), ps[i].width);
-      wr.put((uint64_t)xs[i] ^ ((rs[i] ^ (uint64_t)gi) << ns[i]), ps[i].len);
-    }
-    n = m;
-  } else {
-    encode_plane_step<DIMS>(x0, n, wr);
-    encode_plane_step<DIMS>(x1, n, wr);
-    encode_plane_step<DIMS>(x2, n, wr);
-    encode_plane_step<DIMS>(x3, n, wr);
-  }
-}
-
 // Planes 31 .. cmin of 32-bit half H, two at a time (an odd one left at the
 // bottom goes alone); false once the block is full.
 template <int H, typename UInt, int DIMS, typename Writer>
@@ -936,9 +861,6 @@ ZFP_HD bool encode_half(const planes<UInt, DIMS>& P, unsigned& n, int cmin, Writ
 template <int H, int C, bool PRI = true, typename UInt, int DIMS, typename Writer>
 ZFP_HD bool encode_half_fixed(const planes<UInt, DIMS>& P, unsigned& n, Writer& wr) {
   typedef typename plane_word<DIMS>::type PW;
-#if defined(CUZFP_EXP_TRIPS)  // timing experiment: only the first CUZFP_EXP_TRIPS trips (wrong output)
-  if constexpr (C < 31 - 2 * CUZFP_EXP_TRIPS) return true;
-#endif
   if constexpr (C >= 1) {
     if (!any_lane(!wr.full())) return false;
     wr.settle();
@@ -949,29 +871,8 @@ ZFP_HD bool encode_half_fixed(const planes<UInt, DIMS>& P, unsigned& n, Writer& 
       else if constexpr (C == CUZFP_PRIO_T0) __builtin_amdgcn_s_setprio(0);
     }
 #endif
-#if defined(CUZFP_EXP_ENC4)
-    if constexpr (DIMS == 3 && C % 4 == 3) {
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(CUZFP_NO_PRIO)
-      if constexpr (prio_of<Writer>::value && PRI) {  // the drops that fall inside these 4 planes
-        if constexpr (C >= CUZFP_PRIO_T0 && C - 4 < CUZFP_PRIO_T0) __builtin_amdgcn_s_setprio(0);
-        else if constexpr (C >= CUZFP_PRIO_T1 && C - 4 < CUZFP_PRIO_T1) __builtin_amdgcn_s_setprio(1);
-        else if constexpr (C >= CUZFP_PRIO_T2 && C - 4 < CUZFP_PRIO_T2) __builtin_amdgcn_s_setprio(2);
-      }
-#endif
-      encode_plane_quad_step<DIMS>((PW)P.template get<H>(C), (PW)P.template get<H>(C - 1),
-                                   (PW)P.template get<H>(C - 2), (PW)P.template get<H>(C - 3), n, wr);
-      return encode_half_fixed<H, C - 4, PRI>(P, n, wr);
-    }
-#endif
-#if defined(CUZFP_EXP_ENC2)
-    if constexpr (DIMS == 3) {
-      encode_plane_pair_step<DIMS>((PW)P.template get<H>(C), (PW)P.template get<H>(C - 1), n, wr);
-    } else
-#endif
-    {
-      encode_plane_step<DIMS>((PW)P.template get<H>(C), n, wr);
-      encode_plane_step<DIMS>((PW)P.template get<H>(C - 1), n, wr);
-    }
+    encode_plane_step<DIMS>((PW)P.template get<H>(C), n, wr);
+    encode_plane_step<DIMS>((PW)P.template get<H>(C - 1), n, wr);
     return encode_half_fixed<H, C - 2, PRI>(P, n, wr);
   }
   return true;
@@ -1106,13 +1007,11 @@ ZFP_HD void encode_planes(const planes<UInt, DIMS>& P, unsigned maxprec, Writer&
     // 32-bit coefficients are coded down to plane 0: precision() is 32 for
     // every f32 exponent (emax >= -149), and int32 has maxprec 32
     (void)maxprec;
-#if !defined(CUZFP_EXP_NOPAIR1D)  // (A/B builds: the 1D plane steps without the pair table)
     if constexpr (DIMS == 1 && has_pair1d<Writer>::value) {
       uint32_t n10 = 0;
       encode_pairs_1d<0, 31>(P, n10, wr);
       return;
     }
-#endif
     encode_half_fixed<0, 31>(P, n, wr);
   } else {
     const int kmin = PREC > (int)maxprec ? PREC - (int)maxprec : 0;
@@ -1677,16 +1576,7 @@ ZFP_HD PW decode_plane_fast(unsigned& n, Reader& rd, bool& slow, bool& rare) {
   // v_bfi_b32 a dword under the mask ~0 << nf
   const PW x = merge_at<PW>(nf, ones, w);
   n = nf + npos;
-#if defined(CUZFP_EXP_DEC_EXTRA_RT)  // timing experiment: one more dependent LDS round trip a plane
-  {
-    uint32_t a = nf + used;
-    const uint32_t dummy = rd.window32(rd.pos + a);
-    asm volatile("; dep %1" : "+v"(a) : "v"(dummy));  // the advance waits for the read
-    rd.pos = umin(rd.pos + a, rd.end);
-  }
-#else
   rd.pos = umin(rd.pos + nf + used, rd.end);
-#endif
   return x;
 }
 
@@ -1750,9 +1640,6 @@ ZFP_HD int decode_half(planes<UInt, DIMS>& P, unsigned& n, int cmin, Reader& rd)
   int c = 31;
   for (; c - 1 >= cmin; c -= 2) {
     if (!any_lane(rd.pos < rd.end)) return c;
-#if defined(CUZFP_EXP_DTRIPS)  // timing experiment: only the first CUZFP_EXP_DTRIPS trips (wrong output)
-    if (c < 31 - 2 * CUZFP_EXP_DTRIPS) return c;
-#endif
     if constexpr (prio_of<Reader>::value)
       progress_priority<CUZFP_DPRIO_T2, CUZFP_DPRIO_T1, CUZFP_DPRIO_T0>(uniform(c));
     PW xa, xb;
@@ -1990,29 +1877,6 @@ __device__ __forceinline__ float absmax_nan(const float* f) {
 }
 #endif
 
-#if defined(CUZFP_EXP_PAD) && defined(__HIP_DEVICE_COMPILE__)
-#ifndef CUZFP_EXP_PAD_AT
-#define CUZFP_EXP_PAD_AT 1
-#endif
-// timing experiment (tools/xvar.py): CUZFP_EXP_PAD x 8 independent dummy VALU
-// ops (v_add_u32, or v_bfi_b32 with CUZFP_EXP_PAD_SLOW), at the gathers
-// (CUZFP_EXP_PAD_AT 0) or after the block's exponent (1, the data is in)
-__device__ __forceinline__ void exp_pad(uint32_t seed) {
-  uint32_t d0 = seed, d1 = seed + 1, d2 = seed + 2, d3 = seed + 3, d4 = seed + 4, d5 = seed + 5, d6 = seed + 6,
-           d7 = seed + 7;
-#if defined(CUZFP_EXP_PAD_SLOW)
-#define ZFP_PAD_OP(r) "v_bfi_b32 " r ", %8, " r ", %9\n"
-#else
-#define ZFP_PAD_OP(r) "v_add_u32 " r ", " r ", %9\n"
-#endif
-  asm volatile(".rept %c10\n" ZFP_PAD_OP("%0") ZFP_PAD_OP("%1") ZFP_PAD_OP("%2") ZFP_PAD_OP("%3")
-               ZFP_PAD_OP("%4") ZFP_PAD_OP("%5") ZFP_PAD_OP("%6") ZFP_PAD_OP("%7") ".endr\n"
-               : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3), "+v"(d4), "+v"(d5), "+v"(d6), "+v"(d7)
-               : "s"(0x0f0f0f0fu), "v"(seed * 3u), "i"(CUZFP_EXP_PAD));
-#undef ZFP_PAD_OP
-}
-#endif
-
 template <typename Scalar, int DIMS, typename Writer>
 ZFP_HD void encode_block(const Scalar* f, unsigned maxbits, Writer& wr) {
   typedef traits<Scalar> T;
@@ -2047,9 +1911,6 @@ ZFP_HD void encode_block(const Scalar* f, unsigned maxbits, Writer& wr) {
     const int emax = fp<Scalar>::template emax<N>((const Scalar*)f);
 #endif
     ZFP_STAMP(1);
-#if defined(CUZFP_EXP_PAD) && defined(__HIP_DEVICE_COMPILE__) && CUZFP_EXP_PAD_AT == 1
-    exp_pad((uint32_t)emax);
-#endif
     maxprec = precision<DIMS>(emax, T::prec);
     const unsigned e = maxprec ? (unsigned)(emax + T::ebias) : 0u;
     if (!e) {  // all-zero block: a single 0 bit, then padding

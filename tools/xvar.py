@@ -3,10 +3,10 @@
   python tools/xvar.py build NAME "-DFLAG=1 ..." [NAME "FLAGS" ...]   # here
   python tools/xvar.py isa NAME [NAME ...]                            # here: ISA histograms
   python tools/xvar.py run [--size S] [--field F] [--dims D --rate R] NAME [NAME ...]   # GPU box
-    (variants built with -DCUZFP_EXP_DIMS=D for 1D / 2D)
+    (variants built with -DCUZFP_XVAR_DIMS=D for 1D / 2D)
 
 Unlike tools/variants.py (a full library per variant), a variant here compiles
-only the 3D fast-gather float kernels (-DCUZFP_EXP_ONLY3D); the other scalar
+only the 3D fast-gather float kernels (-DCUZFP_XVAR); the other scalar
 types are stubs built once.  `run` times encode / decode / the step with
 hipGraphs and checks the stream and the decoded array against the reference's
 SHA-256 digests in tests/golden/golden.json (256^3 rate 8, polynomial and
@@ -34,8 +34,8 @@ def _stub_objs(unit):
     os.makedirs(STUB, exist_ok=True)
     hdrs = [os.path.join(b.CSRC, h) for h in b.HEADERS] + [os.path.join(b.INC, "cuzfp_hip.h")]
     objs, procs = [], []
-    for u, flags in (("inst_f32", ["-DCUZFP_EXP_STUB"]), ("inst_f64", ["-DCUZFP_EXP_STUB"]),
-                     ("inst_i32", ["-DCUZFP_EXP_STUB"]), ("inst_i64", ["-DCUZFP_EXP_STUB"]), ("capi", [])):
+    for u, flags in (("inst_f32", ["-DCUZFP_XVAR", "-DCUZFP_XVAR_STUB"]), ("inst_f64", ["-DCUZFP_XVAR", "-DCUZFP_XVAR_STUB"]),
+                     ("inst_i32", ["-DCUZFP_XVAR", "-DCUZFP_XVAR_STUB"]), ("inst_i64", ["-DCUZFP_XVAR", "-DCUZFP_XVAR_STUB"]), ("capi", [])):
         if u == unit:
             continue
         o = os.path.join(STUB, u + ".o")
@@ -59,7 +59,7 @@ def build(pairs):
         os.makedirs(d, exist_ok=True)
         u = _unit(flags)
         fl = [f for f in flags.split() if f != "@f64"]
-        procs.append(subprocess.Popen([b.HIPCC, *b.CXXFLAGS, "-DCUZFP_EXP_ONLY3D", *fl, "-c",
+        procs.append(subprocess.Popen([b.HIPCC, *b.CXXFLAGS, "-DCUZFP_XVAR", *fl, "-c",
                                        os.path.join(b.CSRC, u + ".hip"), "-o", os.path.join(d, "inst_f32.o")]))
     assert all(p.wait() == 0 for p in procs)
     for name, flags in pairs:
