@@ -1877,6 +1877,55 @@ __device__ __forceinline__ float absmax_nan(const float* f) {
 }
 #endif
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// q = (Int)(s * f) for an even number of floats, with the reference's x86 cast
+// (cvttss2si: NaN or |y| >= 2^31 -> INT_MIN).  fast: a block of finite values
+// with a finite scale, where |y| < 2^30 (max |x| < 2^emax), so v_cvt_i32_f32's
+// truncation is the x86 cast and the product pairs go through v_pk_mul_f32;
+// otherwise the exact path (encode.c:35-52, oracle/zfp_oracle.c).
+template <int N>
+__device__ __forceinline__ void quantize_f32(const float* f, float s, bool fast, uint32_t* q) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  if (fast) {
+    const f2 ss = {s, s};
+#pragma unroll
+    for (int i = 0; i < N; i += 2) {
+      const f2 y = f2{f[i], f[i + 1]} * ss;
+      q[i] = (uint32_t)(int32_t)y.x;  // v_cvt_i32_f32 (|y| < 2^30 here)
+      q[i + 1] = (uint32_t)(int32_t)y.y;
+    }
+  }
+  if (fast) {
+  } else {
+    // Two values per statement, in place (tied operands), so the quantised
+    // block reuses the input registers instead of doubling the block's
+    // register footprint.  Each compare result is read >= 2 instructions
+    // after it is written (VALU SGPR/VCC write -> v_cndmask read).
+    const float lim = 2147483648.0f;
+    const uint32_t imin = 0x80000000u;
+#pragma unroll
+    for (int i = 0; i < N; i += 2) {
+      float a = f[i], b = f[i + 1];
+      uint64_t m;
+      uint32_t t;
+      asm("v_mul_f32 %0, %0, %4\n\t"
+          "v_mul_f32 %1, %1, %4\n\t"
+          "v_cmp_gt_f32_e64 vcc, %5, |%0|\n\t"
+          "v_cmp_gt_f32_e64 %2, %5, |%1|\n\t"
+          "v_cvt_i32_f32 %3, %0\n\t"
+          "v_cndmask_b32 %0, %6, %3, vcc\n\t"
+          "v_cvt_i32_f32 %3, %1\n\t"
+          "v_cndmask_b32_e64 %1, %6, %3, %2"
+          : "+v"(a), "+v"(b), "=&s"(m), "=&v"(t)
+          : "v"(s), "v"(lim), "v"(imin)
+          : "vcc");
+      q[i] = __builtin_bit_cast(uint32_t, a);
+      q[i + 1] = __builtin_bit_cast(uint32_t, b);
+    }
+  }
+}
+#endif
+
 template <typename Scalar, int DIMS, typename Writer>
 ZFP_HD void encode_block(const Scalar* f, unsigned maxbits, Writer& wr) {
   typedef traits<Scalar> T;
@@ -1924,49 +1973,8 @@ ZFP_HD void encode_block(const Scalar* f, unsigned maxbits, Writer& wr) {
     // oracle/zfp_oracle.c.
     const Scalar s = (Scalar)fp<Scalar>::pow2(T::prec - 2 - emax);
 #if defined(__HIP_DEVICE_COMPILE__)
-    // Fast path: in a block of finite values with a finite scale, |y| < 2^30
-    // (max |x| < 2^emax), so v_cvt_i32_f32's truncation is the x86 cast and
-    // the product pairs go through v_pk_mul_f32.
-    typedef float f2 __attribute__((ext_vector_type(2)));
-    const bool fast = finite && emax >= -97;
     if constexpr (sizeof(Scalar) == 4 && N % 2 == 0) {
-      if (fast) {
-        const f2 ss = {(float)s, (float)s};
-#pragma unroll
-        for (int i = 0; i < N; i += 2) {
-          const f2 y = f2{(float)f[i], (float)f[i + 1]} * ss;
-          q[i] = (UInt)(int32_t)y.x;  // v_cvt_i32_f32 (|y| < 2^30 here)
-          q[i + 1] = (UInt)(int32_t)y.y;
-        }
-      }
-    }
-    if (fast) {
-    } else if constexpr (sizeof(Scalar) == 4 && N % 2 == 0) {
-      // Two values per statement, in place (tied operands), so the quantised
-      // block reuses the input registers instead of doubling the block's
-      // register footprint.  Each compare result is read >= 2 instructions
-      // after it is written (VALU SGPR/VCC write -> v_cndmask read).
-      const float lim = 2147483648.0f;
-      const uint32_t imin = 0x80000000u;
-#pragma unroll
-      for (int i = 0; i < N; i += 2) {
-        float a = (float)f[i], b = (float)f[i + 1];
-        uint64_t m;
-        uint32_t t;
-        asm("v_mul_f32 %0, %0, %4\n\t"
-            "v_mul_f32 %1, %1, %4\n\t"
-            "v_cmp_gt_f32_e64 vcc, %5, |%0|\n\t"
-            "v_cmp_gt_f32_e64 %2, %5, |%1|\n\t"
-            "v_cvt_i32_f32 %3, %0\n\t"
-            "v_cndmask_b32 %0, %6, %3, vcc\n\t"
-            "v_cvt_i32_f32 %3, %1\n\t"
-            "v_cndmask_b32_e64 %1, %6, %3, %2"
-            : "+v"(a), "+v"(b), "=&s"(m), "=&v"(t)
-            : "v"(s), "v"(lim), "v"(imin)
-            : "vcc");
-        q[i] = __builtin_bit_cast(UInt, a);
-        q[i + 1] = __builtin_bit_cast(UInt, b);
-      }
+      quantize_f32<N>((const float*)f, (float)s, finite && emax >= -97, (uint32_t*)q);
     } else
 #endif
     {
