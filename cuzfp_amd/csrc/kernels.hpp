@@ -23,7 +23,6 @@
 #include <stdlib.h>
 
 #include <atomic>
-#include <type_traits>
 
 #if defined(CUZFP_PROBE) && CUZFP_PROBE == 9
 // Diagnostic build (tools/probe.py stamps): lane 0 of every wave records
@@ -56,7 +55,6 @@ __device__ __forceinline__ void stamp_real(int slot) {
 #endif
 
 #include "zfp_block.hpp"
-#include "split3.hpp"
 #include "launch.hpp"
 
 namespace cuzfp {
@@ -1013,185 +1011,6 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) voi
 }
 
 // ---------------------------------------------------------------------------
-// The lane-pair 3D f32 encoder (split3.hpp): 32 blocks a wave, each coded by
-// lanes l and l + 32; <= 64 VGPRs, 8 waves a SIMD.
-
-// The plane coder's writer for the lane-pair encoder: LdsOrWriter with the put
-// position clamped at the budget.  A full lane's pieces then land whole in the
-// slack row W (a piece put at bit 64 W has no part in row W + 1: it ORs zero
-// there), so a column needs one slack row and the steps need no settle().
-struct LdsClampWriter {
-  static constexpr bool kPrio = false;
-  uint64_t* p;        // the lane's column: word j at p[64 j], W + 1 words, zeroed
-  lds_spread* lut;    // the workgroup's spread tables
-  uint32_t pos, lim;  // bits produced; 64 * W
-  __device__ __forceinline__ bool full() const { return pos >= lim; }
-  __device__ __forceinline__ void put(uint64_t v, unsigned n) {  // v < 2^n
-    const uint32_t at = min(pos, lim);
-    uint64_t* q = p + (at >> 6) * 64;
-    uint64_t lo, hi;
-    asm("v_lshlrev_b64 %0, %1, %2" : "=v"(lo) : "v"(at), "v"(v));
-    asm("v_lshrrev_b64 %0, 1, %1" : "=v"(hi) : "v"(v));
-    asm("v_lshrrev_b64 %0, %1, %0" : "+v"(hi) : "v"(at ^ 63u));
-    atomicOr((unsigned long long*)&q[0], (unsigned long long)lo);
-    atomicOr((unsigned long long*)&q[64], (unsigned long long)hi);
-    pos += n;
-  }
-  __device__ __forceinline__ uint32_t sp0(uint32_t o) const { return *(lds_spread*)((uintptr_t)lut + o); }
-  __device__ __forceinline__ uint32_t sp1(uint32_t o) const { return *(lds_spread*)((uintptr_t)(lut + 256) + o); }
-  __device__ __forceinline__ uint32_t spread(uint32_t b) const { return lut[256 + b] >> 1; }
-  __device__ __forceinline__ void zero_bit() { pos++; }
-  __device__ __forceinline__ void finish() {}
-  __device__ __forceinline__ void settle() {}
-};
-
-constexpr int kSplitWaves = 8;  // waves a workgroup: 2 a SIMD, 4 workgroups a CU at rate 8
-
-// local planes J, J-1 (A: global 16 + J, B: J; lo half in w[16 + J], hi in
-// w[J]) down to 0, while any lane of the wave has budget
-template <int J>
-__device__ __forceinline__ void split_planes(const uint32_t* w, unsigned& n, LdsClampWriter& wr) {
-  if constexpr (J >= 1) {
-    if (!any_lane(!wr.full())) return;
-    encode_plane_step<3>((uint64_t)w[16 + J] | ((uint64_t)w[J] << 32), n, wr);
-    encode_plane_step<3>((uint64_t)w[15 + J] | ((uint64_t)w[J - 1] << 32), n, wr);
-    split_planes<J - 2>(w, n, wr);
-  }
-}
-
-template <bool PRIO = false>  // (a template: instantiated by the float unit alone)
-__global__ __launch_bounds__(kLanes * kSplitWaves, 8) void zfp_encode3_split(const float* __restrict__ data,
-                                                                              Geometry g,
-                                                                              uint64_t* __restrict__ stream) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  extern __shared__ __attribute__((aligned(16))) uint64_t lds_all[];
-  __shared__ __attribute__((aligned(16))) uint32_t stab[512];  // LDS address 0 (static)
-  const uint32_t wig = threadIdx.x >> 6;
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t h = lane >> 5, l = lane & 31;  // half (A = 0, B = 1), block in the wave
-  const uint32_t wave = 2 * g.wave0 + blockIdx.x * kSplitWaves + wig;  // waves of 32 blocks
-  if (wave >= 2 * g.wave_end) return;
-  const uint32_t b = wave * 32 + l;
-  const bool live = b < g.nblocks;
-  uint64_t* lds = lds_all + (size_t)wig * g.lds_words;
-  // the spread tables: loads issued first, stored by every wave (as zfp_encode)
-  uint4 tab16[kSpreadTabBytes / 16 / kLanes];
-#pragma unroll
-  for (uint32_t i = 0; i < kSpreadTabBytes / 16 / kLanes; i++) tab16[i] = ((const uint4*)g_spread_tab.e)[lane + i * kLanes];
-  float f[32];
-  if (live) {
-    const BlockPos bp = block_pos<3>(g, b);
-    const float* p = data + ((size_t)(4 * bp.iz + 2 * h) * g.ny + 4 * bp.iy) * g.nx + 4 * bp.ix;
-#pragma unroll
-    for (int zl = 0; zl < 2; zl++)
-#pragma unroll
-      for (int y = 0; y < 4; y++) load_row(p + ((size_t)zl * g.ny + y) * g.nx, f + 16 * zl + 4 * y);
-  } else {
-#pragma unroll
-    for (int i = 0; i < 32; i++) f[i] = 0.0f;
-  }
-#pragma unroll
-  for (uint32_t i = 0; i < kSpreadTabBytes / 16 / kLanes; i++) ((uint4*)stab)[lane + i * kLanes] = tab16[i];
-  const uint32_t W = g.maxbits >> 6;
-  uint64_t* mine = lds + lane;
-  for (uint32_t j = 0; j <= W; j++) mine[64 * j] = 0;  // own column and its slack row
-  // block exponent (encode.c:9-33) from the two halves' maxima: NaN-propagating
-  // for the finiteness test, the reference's NaN-ignoring maximum otherwise
-  const float mh = absmax_nan<32>(f);
-  const uint2 mm = split3::xboth(__float_as_uint(mh));
-  float mx;
-  asm("v_maximum3_f32 %0, %1, %2, %2" : "=v"(mx) : "v"(__uint_as_float(mm.x)), "v"(__uint_as_float(mm.y)));
-  const bool finite = __builtin_isfinite(mx);
-  int emax;
-  if (__builtin_expect(finite, 1)) {
-    const uint32_t bm = __float_as_uint(mx);
-    emax = bm ? (int)(bm >> 23) - 126 : -127;
-  } else {  // both halves of a block take this branch together
-    float r = 0.0f;
-#pragma unroll
-    for (int i = 0; i < 32; i++) r = fmaxf(r, fabsf(f[i]));
-    const uint2 rr = split3::xboth(__float_as_uint(r));
-    const uint32_t bb = __float_as_uint(fmaxf(__uint_as_float(rr.x), __uint_as_float(rr.y)));
-    const int E = (int)(bb >> 23);
-    emax = bb == 0 ? -127 : E == 255 ? 0 : E - 126;
-  }
-  const uint32_t e = (uint32_t)(emax + 127);  // precision() is 32 for every f32 exponent
-  uint32_t q[32];
-  quantize_f32<32>(f, fp<float>::pow2(30 - emax), finite && emax >= -97, q);
-  split3::lift_xy(q);
-#pragma unroll
-  for (int zl = 0; zl < 2; zl++)
-#pragma unroll
-    for (int i = 0; i < 8; i++) split3::xswap(q[16 * zl + split3::K[i]], q[16 * zl + split3::PI[i]]);
-  split3::lift_z(q);
-#pragma unroll
-  for (int m = 0; m < split3::kMovers; m++) split3::xswap(q[split3::SWAP[m][0]], q[split3::SWAP[m][1]]);
-  // transposition inputs: perm[t] (A) / perm[32 + t] (B), plus the negabinary
-  // offset (its final "^ 0xaaaa..." comes with the transposition, kOddWords)
-  uint32_t w[32];
-#pragma unroll
-  for (int t = 0; t < 32; t++) {
-    constexpr uint32_t NB = 0xaaaaaaaau;
-    const int ra = split3::kLayout.srcA[t], rb = split3::kLayout.srcB[t];
-    w[t] = (ra == rb ? q[ra] : h ? q[rb] : q[ra]) + NB;
-  }
-  transpose_tiles<32, kOddWords>(w);
-  // B's n at its first plane: the reference's n after plane 16
-  uint32_t o = 0;
-#pragma unroll
-  for (int k = 16; k < 32; k++) o |= w[k];
-  const uint2 oo = split3::xboth(o);
-  const uint32_t blh = bitlen16(oo.y), bll = bitlen16(oo.x);  // (v_ffbh-based: any 32-bit word)
-  const uint32_t bl = blh ? 32u + blh : bll;
-  unsigned n = h ? (bl < 63u ? bl : 63u) : 0u;
-#pragma unroll
-  for (int j = 0; j < 16; j++) split3::xswap(w[16 + j], w[j]);
-  // A's planes 31..16 from bit 9, B's planes 15..0 into its own column
-  LdsClampWriter wr{mine, (lds_spread*)stab, 0u, 64u * W};
-  if (!live || e == 0) wr.pos = wr.lim;  // an all-zero block: one 0 bit (the zeroed column)
-  wave_lds_sync();  // the tables and the zeroed columns
-  wr.put(h ? 0ull : 2ull * e + 1, h ? 0u : 9u);
-  split_planes<15>(w, n, wr);
-  // B's bits after A's
-  wave_lds_sync();
-  const uint32_t endA = split3::xboth(wr.pos).x;
-  if (h && endA < wr.lim) {
-    uint64_t* acol = lds + l;
-    const uint32_t left = wr.lim - endA;
-    for (uint32_t j = 0; 64 * j < left; j++) {
-      const uint64_t x = mine[64 * j];
-      const uint32_t d = endA + 64 * j;
-      uint64_t* qd = acol + (d >> 6) * 64;
-      uint64_t lo, hi;
-      asm("v_lshlrev_b64 %0, %1, %2" : "=v"(lo) : "v"(d), "v"(x));
-      asm("v_lshrrev_b64 %0, 1, %1" : "=v"(hi) : "v"(x));
-      asm("v_lshrrev_b64 %0, %1, %0" : "+v"(hi) : "v"(d ^ 63u));
-      atomicOr((unsigned long long*)&qd[0], (unsigned long long)lo);
-      atomicOr((unsigned long long*)&qd[64], (unsigned long long)hi);
-    }
-  }
-  wave_lds_sync();
-  // copy-out: A's column, its first half of the words by A, the rest by B
-  if (live) {
-    const uint64_t* acol = lds + l;
-    uint64_t* dst = stream + (size_t)b * W;
-    const uint32_t H = (W + 1) >> 1, j0 = h * H, j1 = min(W, j0 + H);
-    if (g.vec_io && !(W & 3)) {
-      for (uint32_t j = j0; j < j1; j += 2) {
-        uint4 v;
-        const uint64_t a0 = acol[64 * j], a1 = acol[64 * (j + 1)];
-        __builtin_memcpy(&v.x, &a0, 8);
-        __builtin_memcpy(&v.z, &a1, 8);
-        st16<kNtStream>(&dst[j], v);
-      }
-    } else {
-      for (uint32_t j = j0; j < j1; j++) dst[j] = acol[64 * j];
-    }
-  }
-#endif  // __HIP_DEVICE_COMPILE__
-}
-
-// ---------------------------------------------------------------------------
 // Launchers
 
 // The current device's LDS budget of one workgroup
@@ -1258,16 +1077,6 @@ static inline bool use_priority(uint32_t nwaves, int waves_per_simd, uint32_t ro
   return nwaves <= (uint32_t)c * 4u * (uint32_t)waves_per_simd * rounds;
 }
 
-// The lane-pair 3D f32 encoder (zfp_encode3_split) where it applies; the
-// environment variable CUZFP_SPLIT3=0 (read once a process) selects the
-// one-block-per-lane encoder instead (A/B timing, tests of both kernels).
-static inline bool split3_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("CUZFP_SPLIT3");
-    return !(e && *e && atoi(e) == 0);
-  }();
-  return on;
-}
 #if defined(CUZFP_XVAR)  // tools/xvar.py builds: the fast-gather kernels only (compile time)
 constexpr bool kFastOnly = true;
 #else
@@ -1319,20 +1128,6 @@ int launch_encode_t(const void* data, const Geometry& g, bool fast, uint64_t* st
       else if (prio) ZFP_ENC_REG(false, true);
       else ZFP_ENC_REG(false, false);
 #undef ZFP_ENC_REG
-      const hipError_t e = hipGetLastError();
-      t_last_hip = e;
-      return e == hipSuccess ? CUZFP_SUCCESS : CUZFP_ERROR_HIP;
-    }
-  }
-  // 3D float, contiguous, maxbits a multiple of 64: the lane-pair encoder
-  // (32 blocks a wave) when a workgroup of its waves fits the LDS budget
-  if constexpr (DIMS == 3 && std::is_same<Scalar, float>::value) {
-    const size_t words = (size_t)kLanes * ((g.maxbits >> 6) + 1);  // a wave's columns + slack row
-    const size_t shared = kSplitWaves * words * 8 + kLanes * 8;     // + one row past the last wave
-    if (fast && (g.maxbits & 63) == 0 && split3_enabled() && shared + kSpreadTabBytes <= lds_cap_bytes()) {
-      gg.lds_words = (uint32_t)words;
-      const dim3 grid((2 * nwaves + kSplitWaves - 1) / kSplitWaves), block(kLanes * kSplitWaves);
-      hipLaunchKernelGGL(zfp_encode3_split<false>, grid, block, shared, st, d, gg, stream);
       const hipError_t e = hipGetLastError();
       t_last_hip = e;
       return e == hipSuccess ? CUZFP_SUCCESS : CUZFP_ERROR_HIP;

@@ -13,7 +13,6 @@
 #include <string.h>
 
 #include "../../cuzfp_amd/csrc/zfp_block.hpp"
-#include "../../cuzfp_amd/csrc/split3.hpp"
 
 namespace {
 
@@ -103,82 +102,6 @@ int emu_decompress(int type, unsigned nx, unsigned ny, unsigned nz, long long sx
 }  // extern "C"
 
 
-// The lane-pair 3D f32 encoder (cuzfp_amd/csrc/split3.hpp) on the host: the
-// two halves of a block as two register files, the kernel's v_permlane32_swap
-// exchanges done on them directly, each half's plane coder with its own
-// writer (A from bit 9 of the block, B into a scratch block from bit 0), then
-// B's bits appended at A's end position.  Same stages and tables as the
-// kernel; the quantisation is the reference's (the kernels' is checked by
-// encode_block's emulation).
-namespace {
-using namespace cuzfp;
-
-// vdst = (a0 | b0), vsrc = (a1 | b1) -> vdst = (a0 | a1), vsrc = (b0 | b1)
-void host_swap(uint32_t* A, uint32_t* B, int v0, int v1) {
-  const uint32_t a0 = A[v0], b0 = B[v0], a1 = A[v1], b1 = B[v1];
-  A[v0] = a0, B[v0] = a1, A[v1] = b0, B[v1] = b1;
-}
-
-unsigned bitlen64(uint64_t x) { return x ? 64u - (unsigned)__builtin_clzll(x) : 0u; }
-
-void encode_block_split3(const float* blk, unsigned maxbits, uint64_t* out /* zeroed, maxbits bits */) {
-  const int emax = fp<float>::emax<64>(blk);
-  const unsigned e = (unsigned)(emax + 127);  // precision() is 32 for every f32 exponent
-  if (!e) return;                             // all-zero block: one 0 bit, then padding
-  const float s = fp<float>::pow2(30 - emax);
-  uint32_t A[32], B[32];
-  for (int zl = 0; zl < 2; zl++)
-    for (int i = 0; i < 16; i++) {
-      A[zl * 16 + i] = (uint32_t)fp<float>::to_int(s * blk[16 * zl + i]);
-      B[zl * 16 + i] = (uint32_t)fp<float>::to_int(s * blk[16 * (2 + zl) + i]);
-    }
-  split3::lift_xy(A);
-  split3::lift_xy(B);
-  for (int zl = 0; zl < 2; zl++)
-    for (int i = 0; i < 8; i++) host_swap(A, B, 16 * zl + split3::K[i], 16 * zl + split3::PI[i]);
-  split3::lift_z(A);
-  split3::lift_z(B);
-  for (int m = 0; m < split3::kMovers; m++) host_swap(A, B, split3::SWAP[m][0], split3::SWAP[m][1]);
-  uint32_t wa[32], wb[32];
-  for (int t = 0; t < 32; t++) {
-    wa[t] = A[split3::kLayout.srcA[t]] + 0xaaaaaaaau;
-    wb[t] = B[split3::kLayout.srcB[t]] + 0xaaaaaaaau;
-  }
-  transpose_tiles<32, kOddWords>(wa);
-  transpose_tiles<32, kOddWords>(wb);
-  uint32_t oa = 0, ob = 0;
-  for (int k = 16; k < 32; k++) oa |= wa[k], ob |= wb[k];
-  const unsigned bl = bitlen64((uint64_t)oa | ((uint64_t)ob << 32));
-  for (int j = 0; j < 16; j++) host_swap(wa, wb, 16 + j, j);
-  uint64_t sb[64] = {};  // B's scratch (maxbits <= 4096 here)
-  HostWriter wra{out, 0, maxbits}, wrb{sb, 0, maxbits};
-  wra.put(2ull * e + 1, 9);
-  unsigned na = 0, nb = bl < 63 ? bl : 63;
-  for (int j = 15; j >= 0; j--) {
-    encode_plane_step<3>((uint64_t)wa[16 + j] | ((uint64_t)wa[j] << 32), na, wra);
-    encode_plane_step<3>((uint64_t)wb[16 + j] | ((uint64_t)wb[j] << 32), nb, wrb);
-  }
-  // B's bits after A's: what fits the block
-  HostWriter wm{out, wra.pos, maxbits};
-  for (unsigned i = 0; i < maxbits && !wm.full(); i += 64) wm.put(sb[i >> 6], 64);
-}
-}  // namespace
-
-extern "C" size_t emu_compress_split3(unsigned nx, unsigned ny, unsigned nz, unsigned maxbits, const float* data,
-                                      uint64_t* stream, size_t bytes) {
-  if (nx % 4 || ny % 4 || nz % 4 || maxbits % 64 || maxbits > 4096) return 0;
-  const size_t bx = nx / 4, by = ny / 4, bz = nz / 4, nb = bx * by * bz, W = maxbits / 64;
-  if (bytes < nb * W * 8) return 0;
-  memset(stream, 0, nb * W * 8);
-  for (size_t b = 0; b < nb; b++) {
-    const size_t ix = b % bx, iy = (b / bx) % by, iz = b / (bx * by);
-    float blk[64];
-    for (int i = 0; i < 64; i++)
-      blk[i] = data[((4 * iz + (i >> 4)) * ny + 4 * iy + ((i >> 2) & 3)) * nx + 4 * ix + (i & 3)];
-    encode_block_split3(blk, maxbits, stream + b * W);
-  }
-  return nb * W * 8;
-}
 
 // Differential fuzz of one plane step: the table decoder (decode_plane_any, the
 // kernels' path) against the general decoder (decode_plane, itself checked

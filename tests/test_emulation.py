@@ -16,7 +16,6 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "tests", "native", "emulate.cpp")
 HDR = os.path.join(ROOT, "cuzfp_amd", "csrc", "zfp_block.hpp")
-HDR3 = os.path.join(ROOT, "cuzfp_amd", "csrc", "split3.hpp")
 HOST_IO = os.path.join(ROOT, "tests", "native", "host_io.hpp")
 LIB = os.path.join(ROOT, "build", "libcuzfp_emu.so")
 TC = {np.dtype(np.int32): 1, np.dtype(np.int64): 2, np.dtype(np.float32): 3, np.dtype(np.float64): 4}
@@ -25,7 +24,7 @@ TC = {np.dtype(np.int32): 1, np.dtype(np.int64): 2, np.dtype(np.float32): 3, np.
 @pytest.fixture(scope="module")
 def emu():
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
-    if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(f) for f in (SRC, HDR, HDR3, HOST_IO)):
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(f) for f in (SRC, HDR, HOST_IO)):
         subprocess.check_call(["/opt/rocm/llvm/bin/clang++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wno-unknown-pragmas",
                                "-o", LIB, SRC])
     lib = ctypes.CDLL(LIB)
@@ -34,8 +33,6 @@ def emu():
     lib.emu_compress.argtypes = args + [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
     lib.emu_decompress.restype = ctypes.c_int
     lib.emu_decompress.argtypes = args + [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
-    lib.emu_compress_split3.restype = ctypes.c_size_t
-    lib.emu_compress_split3.argtypes = [ctypes.c_uint] * 4 + [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
     return lib
 
 
@@ -213,33 +210,3 @@ def test_block_index_division_magic(tmp_path):
     out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0 and out.stdout.strip() == "0", out.stdout + out.stderr
 
-
-def test_split3_encoder_vs_oracle(emu, restatement):
-    """The lane-pair 3D f32 encoder (cuzfp_amd/csrc/split3.hpp, kernel
-    zfp_encode3_split): its stages and layout tables run on two host register
-    files -- the halves' x/y lifts, the z exchange, the mover swaps, the
-    transposition sources, B's starting n from the OR of planes 31..16, the two
-    plane coders and the merge -- against the oracle's stream, on smooth,
-    random, huge-range, sparse, denormal, zero and inf blocks at maxbits 64 ..
-    4096 (the kernel takes multiples of 64)."""
-    rng = np.random.default_rng(33)
-    cases = []
-    for kind in range(4):
-        for _ in range(3):
-            cases.append(_rand(rng, (8, 12, 16), np.float32, kind))
-    for sc in (1e-30, 1e-38, 1e-44, 3e38):
-        a = (rng.standard_normal((8, 8, 8)) * sc).astype(np.float32)
-        a.flat[::5] = 0
-        cases.append(a)
-    cases.append(np.zeros((8, 8, 8), np.float32))
-    inf = rng.standard_normal((8, 8, 8)).astype(np.float32)
-    inf[0, 0, 0] = np.inf
-    cases.append(inf)
-    for a in cases:
-        nz, ny, nx = a.shape
-        nb = (nx // 4) * (ny // 4) * (nz // 4)
-        for mb in (64, 128, 512, 576, 1024, 2048, 4096, int(64 * rng.integers(1, 64))):
-            ref = restatement.compress(a, mb)
-            got = np.zeros(nb * mb // 64, np.uint64)
-            assert emu.emu_compress_split3(nx, ny, nz, mb, a.ctypes.data, got.ctypes.data, got.nbytes) == got.nbytes
-            assert np.array_equal(got, ref), (a.shape, mb)
