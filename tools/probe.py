@@ -42,7 +42,11 @@ def build():
     print("built", OUT)
 
 
-def run(size, field, reps=20):
+def _shape(size, dims):
+    return "(" + ",".join([str(size)] * dims) + ",)"
+
+
+def run(size, field, dims=3, rate=8.0, reps=20):
     res = {}
     for v in (0, 1, 2):
         lib = os.path.join(OUT, f"p{v}", "libcuzfp_hip.so")
@@ -52,10 +56,10 @@ sys.path.insert(0, {ROOT!r})
 os.environ['CUZFP_HIP_LIB'] = {lib!r}
 import cuzfp_amd as cz
 from cuzfp_amd.datagen import polynomial_field, splitmix_uniform
-shape = ({size},)*3
+shape = {_shape(size, dims)}
 arr = polynomial_field(shape) if {field!r} == 'polynomial' else splitmix_uniform(shape)
 x = torch.from_numpy(arr).cuda()
-mb = cz.rate_to_maxbits(8, arr.dtype, 3)
+mb = cz.rate_to_maxbits({rate}, arr.dtype, {dims})
 w = cz.encode(x, mb); y = cz.decode(w, shape, x.dtype, mb)
 def t(fn):
     for _ in range(3): fn()
@@ -80,13 +84,13 @@ sys.path.insert(0, @ROOT@)
 os.environ['CUZFP_HIP_LIB'] = @LIB@
 import cuzfp_amd as cz
 from cuzfp_amd.datagen import polynomial_field, splitmix_uniform
-shape = (@SIZE@,)*3
+shape = @SHAPE@
 arr = polynomial_field(shape) if @FIELD@ == 'polynomial' else splitmix_uniform(shape)
 x = torch.from_numpy(arr).cuda()
-mb = cz.rate_to_maxbits(8, arr.dtype, 3)
+mb = cz.rate_to_maxbits(@RATE@, arr.dtype, @DIMS@)
 lib = cz.library()
 w = cz.encode(x, mb); y = cz.decode(w, shape, x.dtype, mb)
-nw = (@SIZE@ // 4) ** 3 // 64
+nw = min((@SIZE@ // 4) ** @DIMS@ // 64, 65536)
 out = {}
 for name, fn in (("encode", lambda: cz.encode(x, mb, out=w)), ("decode", lambda: cz.decode(w, shape, x.dtype, mb, out=y))):
     for _ in range(3): fn()
@@ -102,10 +106,11 @@ print("ok")
 """
 
 
-def stamps(size, field, outdir, back=1):
+def stamps(size, field, outdir, back=1, dims=3, rate=8.0):
     lib = os.path.join(OUT, "p9", "libcuzfp_hip.so")
     code = STAMP_CODE.replace("@ROOT@", repr(ROOT)).replace("@LIB@", repr(lib)).replace("@SIZE@", str(size)) \
-        .replace("@FIELD@", repr(field)).replace("@OUTDIR@", repr(outdir)).replace("@BACK@", str(back))
+        .replace("@FIELD@", repr(field)).replace("@OUTDIR@", repr(outdir)).replace("@BACK@", str(back)) \
+        .replace("@SHAPE@", _shape(size, dims)).replace("@DIMS@", str(dims)).replace("@RATE@", str(rate))
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     if r.returncode:
         print(r.stderr[-3000:])
@@ -150,12 +155,14 @@ if __name__ == "__main__":
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--field", default="polynomial")
     ap.add_argument("--back", type=int, default=1, help="stamped launches back to back (the last one's stamps)")
+    ap.add_argument("--dims", type=int, default=3)
+    ap.add_argument("--rate", type=float, default=8.0)
     a = ap.parse_args()
     if a.cmd == "build":
         build()
     elif a.cmd == "stamps":
         od = os.path.join(ROOT, "gpurun_out")
         os.makedirs(od, exist_ok=True)
-        stamps(a.size, a.field, od, a.back)
+        stamps(a.size, a.field, od, a.back, a.dims, a.rate)
     else:
-        run(a.size, a.field)
+        run(a.size, a.field, a.dims, a.rate)
