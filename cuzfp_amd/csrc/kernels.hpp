@@ -23,6 +23,7 @@
 #include <stdlib.h>
 
 #include <atomic>
+#include <type_traits>
 
 #if defined(CUZFP_PROBE) && CUZFP_PROBE == 9
 // Diagnostic build (tools/probe.py stamps): lane 0 of every wave records
@@ -200,6 +201,45 @@ struct RegWriter {
   __device__ __forceinline__ uint64_t bits() const { return acc & lowmask(mb); }
 };
 
+// maxbits 32 for floating-point blocks: a coded block's first stream bit is
+// the low bit of its exponent field 2e + 1, always one, so the writer keeps
+// stream bits 1 .. 32 in a 32-bit register at bit positions 0 .. 31 and the
+// count one less than the bits produced.  Every put then shifts by at most 31
+// (a 32-bit shift: the 64-bit one is a slow-issue VALU instruction), a full
+// lane's further bits land at position 31 (stream bit 32, dropped by bits())
+// or beyond (gone), and a zero block (no head()) stays all zeros.  Integer
+// blocks, which have no exponent, keep RegWriter.
+template <bool PRIO = true>
+struct RegWriter32 {
+  static constexpr bool kPrio = PRIO;
+  static constexpr bool kPut32 = true;  // put() keeps the low 32 bits of its value
+  lds_spread* lut;
+  P1dPtr p1d;
+  uint32_t acc, cnt;  // stream bits 1 .., at bit 0 ..; bits produced - 1 (0 before the exponent)
+  __device__ __forceinline__ bool full() const { return cnt >= 31u; }
+  __device__ __forceinline__ void head(uint64_t v, unsigned n) {  // the exponent field, v odd
+    acc = (uint32_t)(v >> 1);
+    cnt = n - 1u;
+  }
+  __device__ __forceinline__ void put(uint32_t v, unsigned n) {
+    acc |= v << cnt;
+    cnt = umin(cnt + n, 31u);
+  }
+  __device__ __forceinline__ void zero_bit() { cnt = umin(cnt + 1u, 31u); }
+  __device__ __forceinline__ uint32_t sp0(uint32_t o) const { return *(lds_spread*)((uintptr_t)lut + o); }
+  __device__ __forceinline__ uint32_t sp1(uint32_t o) const { return *(lds_spread*)((uintptr_t)(lut + 256) + o); }
+  __device__ __forceinline__ uint32_t spread(uint32_t b) const { return lut[256 + b] >> 1; }
+  __device__ __forceinline__ uint32_t pair1d(uint32_t o) const { return *(P1dPtr)((uintptr_t)p1d + o); }
+  __device__ __forceinline__ void finish() {}
+  __device__ __forceinline__ void settle() {}
+  __device__ __forceinline__ uint64_t bits() const { return cnt ? (acc << 1) | 1u : 0u; }
+};
+
+// the register writer of a maxbits-32 (REG 1) / 64 (REG 2) block
+template <typename Scalar, bool PRIO, int REG>
+using reg_writer = typename std::conditional<REG == 1 && !traits<Scalar>::is_int, RegWriter32<PRIO>,
+                                             RegWriter<PRIO, REG == 2>>::type;
+
 // Reader over the lane's block in the wave's lane-interleaved LDS image
 // (dword j of the block at lds32[64 * j]; pos counts bits from the block's
 // start).  The table decoder reads its windows fresh per plane; the general
@@ -345,10 +385,18 @@ struct LdsReader {
 // maxbits, read straight from HBM.  The windows are shifts of it, so a plane
 // step waits on one LDS round trip (the chunk tables) instead of two, and
 // there is no LDS stream image to fill.
-template <bool PRIO = true>
+// B32: a block of at most 32 bits (maxbits <= 32: BASELINE's 1D rate 8 and 2D
+// rate 2).  Its read positions stay below 64 (pos <= 32 plus a window offset
+// < 16), so a window is one 64-bit shift of the zero-extended block, without
+// the bounds test and selects a block of up to 64 bits needs (five of the
+// plane step's slow-issue VALU instructions).
+template <bool PRIO = true, bool B32 = false>
 struct RegReader : LdsReader<PRIO> {
   uint64_t blk;
-  __device__ __forceinline__ uint64_t at(uint32_t p) const { return p < 64 ? blk >> p : 0ull; }
+  __device__ __forceinline__ uint64_t at(uint32_t p) const {
+    if constexpr (B32) return blk >> p;
+    return p < 64 ? blk >> p : 0ull;
+  }
   __device__ __forceinline__ void windows(uint32_t m, uint64_t& w, uint32_t& g) const {
     w = at(this->pos);
     g = (uint32_t)at(this->pos + m);
@@ -684,7 +732,8 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS, true>::value
     wave_lds_sync();  // the spread tables
     uint64_t bits = 0;
     if (b < g.nblocks) {
-      RegWriter<PRIO, REG == 2> wr{lut, p1d, 0, 0, g.maxbits};
+      reg_writer<Scalar, PRIO, REG> wr{lut, p1d, 0, 0};
+      if constexpr (REG == 2 || traits<Scalar>::is_int) wr.mb = g.maxbits;
       encode_block<Scalar, DIMS>(f, g.maxbits, wr);
       bits = wr.bits();
     }
@@ -747,7 +796,9 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS, true>::value
 
 // WPG: waves per workgroup (16 for the 1D register-reader kernel, whose
 // workgroup copies 20 KiB of tables for 1 KiB of output a wave)
-template <typename Scalar, int DIMS, bool FAST, bool PRIO = true, bool REG = false, int WPG = kDecWaves>
+// REG: 0 = the LDS image; 32 / 64 = a block of at most that many bits, read
+// into a register (RegReader)
+template <typename Scalar, int DIMS, bool FAST, bool PRIO = true, int REG = 0, int WPG = kDecWaves>
 __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) void zfp_decode(const uint64_t* __restrict__ stream,
                                                                       Geometry g,
                                                                       Scalar* __restrict__ data) {
@@ -859,7 +910,7 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) voi
     Scalar f[N];
     bool coded;
     if constexpr (REG) {
-      RegReader<PRIO> rd;
+      RegReader<PRIO, REG == 32> rd;
       rd.lds32 = L;
       rd.lut32 = lut;
       rd.d1d = dtab;
@@ -926,7 +977,8 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS, true>::value
     uint64_t bits = 0;
     if (b < g.nblocks) {
       if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);
-      RegWriter<PRIO, REG == 2> wr{lut, p1d, 0, 0, g.maxbits};
+      reg_writer<Scalar, PRIO, REG> wr{lut, p1d, 0, 0};
+      if constexpr (REG == 2 || traits<Scalar>::is_int) wr.mb = g.maxbits;
       encode_block<Scalar, DIMS>(f[k], g.maxbits, wr);
       bits = wr.bits();
     }
@@ -961,7 +1013,7 @@ __device__ __forceinline__ uint64_t reg_block(const uint64_t* stream, const Geom
          lowmask(g.maxbits);
 }
 
-template <typename Scalar, int DIMS, bool FAST, bool PRIO, int WPG, int K>
+template <typename Scalar, int DIMS, bool FAST, bool PRIO, int WPG, int K, int REG = 64>
 __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) void zfp_decode_regk(
     const uint64_t* __restrict__ stream, Geometry g, Scalar* __restrict__ data) {
   static_assert(DIMS <= 2 && K >= 2 && K <= 8, "register-reader batches: 1D/2D, 2-8 a wave");
@@ -993,7 +1045,7 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) voi
     if (b < g.nblocks) {
       if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);  // lowered through the plane loop (progress_priority)
       Scalar f[N];
-      RegReader<PRIO> rd;
+      RegReader<PRIO, REG == 32> rd;
       rd.lds32 = nullptr;
       rd.lut32 = ctab;
       rd.d1d = dtab;
@@ -1185,10 +1237,11 @@ int launch_decode_t(const uint64_t* stream, const Geometry& g, bool fast, void* 
           constexpr int W = kRegBatchWaves1d, K = kRegDecBatch1d;
           const uint32_t phys = (nwaves + K - 1) / K;
           const dim3 kgrid((phys + W - 1) / W), kblock(kLanes * W);
-          if (CUZFP_REG_BATCH_PRIO)
-            hipLaunchKernelGGL((zfp_decode_regk<Scalar, DIMS, true, true, W, K>), kgrid, kblock, 0, st, stream, gg, d);
+          constexpr bool P = CUZFP_REG_BATCH_PRIO;
+          if (g.maxbits <= 32)
+            hipLaunchKernelGGL((zfp_decode_regk<Scalar, DIMS, true, P, W, K, 32>), kgrid, kblock, 0, st, stream, gg, d);
           else
-            hipLaunchKernelGGL((zfp_decode_regk<Scalar, DIMS, true, false, W, K>), kgrid, kblock, 0, st, stream, gg, d);
+            hipLaunchKernelGGL((zfp_decode_regk<Scalar, DIMS, true, P, W, K, 64>), kgrid, kblock, 0, st, stream, gg, d);
           const hipError_t e = hipGetLastError();
           t_last_hip = e;
           return e == hipSuccess ? CUZFP_SUCCESS : CUZFP_ERROR_HIP;
@@ -1196,14 +1249,21 @@ int launch_decode_t(const uint64_t* stream, const Geometry& g, bool fast, void* 
       }
       constexpr int W = DIMS == 1 ? kRegWaves1d : kRegWaves2d;
       const dim3 rgrid((nwaves + W - 1) / W), rblock(kLanes * W);
-      if (fast && prio)
-        hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, true, true, true, W>), rgrid, rblock, 0, st, stream, gg, d);
-      else if (fast)
-        hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, true, false, true, W>), rgrid, rblock, 0, st, stream, gg, d);
-      else if (prio)
-        hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, false, true, true, W>), rgrid, rblock, 0, st, stream, gg, d);
+      auto go = [&](auto rb) {
+        constexpr int RB = decltype(rb)::value;
+        if (fast && prio)
+          hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, true, true, RB, W>), rgrid, rblock, 0, st, stream, gg, d);
+        else if (fast)
+          hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, true, false, RB, W>), rgrid, rblock, 0, st, stream, gg, d);
+        else if (prio)
+          hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, false, true, RB, W>), rgrid, rblock, 0, st, stream, gg, d);
+        else
+          hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, false, false, RB, W>), rgrid, rblock, 0, st, stream, gg, d);
+      };
+      if (g.maxbits <= 32)
+        go(std::integral_constant<int, 32>{});
       else
-        hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, false, false, true, W>), rgrid, rblock, 0, st, stream, gg, d);
+        go(std::integral_constant<int, 64>{});
       const hipError_t e = hipGetLastError();
       t_last_hip = e;
       return e == hipSuccess ? CUZFP_SUCCESS : CUZFP_ERROR_HIP;

@@ -589,6 +589,24 @@ template <typename T> struct prio_of<T, decltype((void)T::kPrio)> {
   static constexpr bool value = T::kPrio;
 };
 
+// Writers whose put() keeps only the low 32 bits of its value (kPut32: the
+// register writer of a 32-bit block), and the exponent field's put (head(),
+// where a writer has one)
+template <typename T, typename = void> struct put32_of {
+  static constexpr bool value = false;
+};
+template <typename T> struct put32_of<T, decltype((void)T::kPut32)> {
+  static constexpr bool value = T::kPut32;
+};
+template <typename W>
+ZFP_HD auto wr_head(W& wr, uint64_t v, unsigned n) -> decltype(wr.head(v, n)) {
+  wr.head(v, n);
+}
+template <typename W, typename... Ignored>
+ZFP_HD void wr_head(W& wr, uint64_t v, unsigned n, Ignored...) {
+  wr.put(v, n);
+}
+
 template <int T2, int T1, int T0>
 ZFP_HD void progress_priority(int c) {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(CUZFP_NO_PRIO)
@@ -747,10 +765,16 @@ ZFP_HD void encode_plane_one_put(PW x, unsigned nf, uint64_t r, const PlaneLen& 
   uint32_t G = e0 >> 5;
   if constexpr (N > 4) G |= wr.sp1(byte_off4<1>(rl)) << (e0 & 31u);
   const uint32_t g = low_bits(G, width);
-  // r < 2^32 here, so r ^ g is (r's high word, rl ^ g): the shift takes r's
-  // register pair as it is instead of a zero-extended copy of rl ^ g
-  const uint64_t code = (uint64_t)x ^ ((r ^ (uint64_t)g) << nf);
-  wr.put(code, pl.len);
+  if constexpr (N <= 16 && put32_of<Writer>::value) {
+    // the writer keeps 32 bits of the code (a 32-bit block: the rest lies past
+    // its end), and r < 2^16: 32-bit shifts
+    wr.put((uint32_t)x ^ ((rl ^ g) << nf), pl.len);
+  } else {
+    // r < 2^32 here, so r ^ g is (r's high word, rl ^ g): the shift takes r's
+    // register pair as it is instead of a zero-extended copy of rl ^ g
+    const uint64_t code = (uint64_t)x ^ ((r ^ (uint64_t)g) << nf);
+    wr.put(code, pl.len);
+  }
   n = pl.nn - pl.imp;  // min(nn, N-1)
 }
 
@@ -811,7 +835,8 @@ template <int DIMS, typename PW, typename Writer>
 ZFP_HD void encode_plane_step(PW x, unsigned& n, Writer& wr) {
   constexpr unsigned N = 1u << (2 * DIMS);
   const unsigned nf = n;  // both steps keep n <= N-1
-  const uint64_t r = (uint64_t)x >> nf;
+  // (16-coefficient planes: a 32-bit shift, nf <= 15)
+  const uint64_t r = N <= 16 ? (uint64_t)((uint32_t)x >> nf) : (uint64_t)x >> nf;
   const uint32_t rl = (uint32_t)r;
   const uint32_t bl = bitlen16(rl);
   const uint32_t L = (uint32_t)__builtin_popcount(rl) + bl;  // v_bcnt_u32_b32(rl, bl)
@@ -1306,12 +1331,14 @@ ZFP_HD uint64_t lowmask64(unsigned m) { return m ? ~0ull >> ((64u - m) & 63u) : 
 // shifted ones in after the insert: two more instructions)
 template <typename PW>
 ZFP_HD PW merge_at(uint32_t s, uint64_t ones, uint64_t w) {
-  const uint64_t hi = ~0ull << s, o = ones << s;
-  if constexpr (sizeof(PW) == 8)
+  if constexpr (sizeof(PW) == 8) {
+    const uint64_t hi = ~0ull << s, o = ones << s;
     return (PW)bfi_v((uint32_t)hi, (uint32_t)o, (uint32_t)w) |
            ((PW)bfi_v((uint32_t)(hi >> 32), (uint32_t)(o >> 32), (uint32_t)(w >> 32)) << 32);
-  else
-    return (PW)bfi_v((uint32_t)hi, (uint32_t)o, (uint32_t)w);
+  } else {
+    // 16-bit planes (2D: s <= 15, ones below bit 16 - s): 32-bit shifts
+    return (PW)bfi_v(~0u << s, (uint32_t)ones << s, (uint32_t)w);
+  }
 }
 
 // (a & m) | c in one v_and_or_b32
@@ -1966,7 +1993,7 @@ ZFP_HD void encode_block(const Scalar* f, unsigned maxbits, Writer& wr) {
       wr.finish();
       return;
     }
-    wr.put(2ull * e + 1, T::ebits + 1);
+    wr_head(wr, 2ull * e + 1, T::ebits + 1);
     // q = (Int)(2^sh * x) with the reference's x86 cast: NaN or |y| >= 2^(p-1)
     // gives INT_MIN.  That happens when 2^sh overflows (max |x| < 2^-97 for
     // f32, 2^-961 for f64) and in blocks holding inf or NaN; see
