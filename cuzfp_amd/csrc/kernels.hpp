@@ -796,8 +796,8 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS, true>::value
 
 // WPG: waves per workgroup (16 for the 1D register-reader kernel, whose
 // workgroup copies 20 KiB of tables for 1 KiB of output a wave)
-// REG: 0 = the LDS image; 32 / 64 = a block of at most that many bits, read
-// into a register (RegReader)
+// REG: 0 = the LDS image; 32 = a block of exactly 32 bits (one dword of the
+// stream), 64 = of at most 64 bits, read into a register (RegReader)
 template <typename Scalar, int DIMS, bool FAST, bool PRIO = true, int REG = 0, int WPG = kDecWaves>
 __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) void zfp_decode(const uint64_t* __restrict__ stream,
                                                                       Geometry g,
@@ -831,7 +831,13 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) voi
   const uint32_t* seg = (const uint32_t*)(stream + (size_t)wave * g.maxbits);
   uint32_t* L = (uint32_t*)lds + lane;
   uint64_t blk = 0;
-  if constexpr (REG) {
+  if constexpr (REG == 32) {
+    // maxbits 32: the lane's block is dword `lane` of the wave's segment
+    if (live) blk = seg[lane];
+    for (uint32_t i = threadIdx.x; i < kLutEnd; i += blockDim.x)
+      ((uint4*)lut)[i] = ((const uint4*)g_chunk_lut.e)[i];
+    copy_dtab();
+  } else if constexpr (REG) {
     // bits [s0, s0 + maxbits) of the wave's segment; dwords past its last one
     // read as zero
     if (live) {
@@ -1006,9 +1012,13 @@ __device__ __forceinline__ uint64_t reg_block(const uint64_t* stream, const Geom
   const uint32_t nb = min((uint32_t)kLanes, g.nblocks - wave * kLanes);
   const uint32_t lim = ((nb * g.maxbits + 63) >> 6) * 2;
   const uint32_t s0 = lane * g.maxbits, d0 = s0 >> 5;
+  // clamped addresses and selects rather than guarded loads: no branch, so
+  // the K batches' loads are all in flight before the first wait
   const uint32_t a0 = seg[d0];
-  const uint32_t a1 = d0 + 1 < lim ? seg[d0 + 1] : 0u;
-  const uint32_t a2 = d0 + 2 < lim ? seg[d0 + 2] : 0u;
+  uint32_t a1 = seg[min(d0 + 1, lim - 1)];
+  uint32_t a2 = seg[min(d0 + 2, lim - 1)];
+  a1 = d0 + 1 < lim ? a1 : 0u;
+  a2 = d0 + 2 < lim ? a2 : 0u;
   return ((uint64_t)__builtin_amdgcn_alignbit(a1, a0, s0) | ((uint64_t)__builtin_amdgcn_alignbit(a2, a1, s0) << 32)) &
          lowmask(g.maxbits);
 }
@@ -1027,7 +1037,10 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) voi
 #pragma unroll
   for (int k = 0; k < K; k++) {
     const uint32_t w = w0 + k;
-    q[k] = (w < g.wave_end && w * kLanes + lane < g.nblocks) ? reg_block(stream, g, w, lane) : 0ull;
+    if (w < g.wave_end && w * kLanes + lane < g.nblocks)
+      q[k] = REG == 32 ? (uint64_t)((const uint32_t*)(stream + (size_t)w * g.maxbits))[lane] : reg_block(stream, g, w, lane);
+    else
+      q[k] = 0;
   }
   constexpr uint32_t kLutEnd = DIMS == 1 ? kLutPairs * 4 / 16 : sizeof(ChunkLut) / 16;
   for (uint32_t i = threadIdx.x; i < kLutEnd; i += blockDim.x) ((uint4*)ctab)[i] = ((const uint4*)g_chunk_lut.e)[i];
@@ -1238,7 +1251,7 @@ int launch_decode_t(const uint64_t* stream, const Geometry& g, bool fast, void* 
           const uint32_t phys = (nwaves + K - 1) / K;
           const dim3 kgrid((phys + W - 1) / W), kblock(kLanes * W);
           constexpr bool P = CUZFP_REG_BATCH_PRIO;
-          if (g.maxbits <= 32)
+          if (g.maxbits == 32)
             hipLaunchKernelGGL((zfp_decode_regk<Scalar, DIMS, true, P, W, K, 32>), kgrid, kblock, 0, st, stream, gg, d);
           else
             hipLaunchKernelGGL((zfp_decode_regk<Scalar, DIMS, true, P, W, K, 64>), kgrid, kblock, 0, st, stream, gg, d);
@@ -1260,7 +1273,7 @@ int launch_decode_t(const uint64_t* stream, const Geometry& g, bool fast, void* 
         else
           hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, false, false, RB, W>), rgrid, rblock, 0, st, stream, gg, d);
       };
-      if (g.maxbits <= 32)
+      if (g.maxbits == 32)
         go(std::integral_constant<int, 32>{});
       else
         go(std::integral_constant<int, 64>{});
