@@ -403,7 +403,12 @@ struct RegReader : LdsReader<PRIO> {
   }
   __device__ __forceinline__ uint64_t peek() const { return at(this->pos); }
   __device__ __forceinline__ uint32_t window32(uint32_t q) const { return (uint32_t)at(q); }
-  __device__ __forceinline__ uint32_t bits8() const { return (uint32_t)(blk >> (this->pos & 63)) & 0xffu; }
+  // (B32: pos <= 32, and at pos = 32 the budget is spent, so the lookup is
+  // the c = 0 entry whatever the bits; v_bfe_u32 reads bits past 31 as zeros)
+  __device__ __forceinline__ uint32_t bits8() const {
+    if constexpr (B32) return __builtin_amdgcn_ubfe((uint32_t)blk, this->pos, 8u);
+    return (uint32_t)(blk >> (this->pos & 63)) & 0xffu;
+  }
   __device__ __forceinline__ void peek2(uint64_t& a, uint64_t& b) const {
     a = at(this->pos);
     b = 0;  // bits past 64: past the block

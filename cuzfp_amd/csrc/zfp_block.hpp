@@ -985,7 +985,7 @@ constexpr void plane_decode_1d(uint32_t s, uint32_t c, uint32_t& n, uint32_t& x,
   used = c - bits;
 }
 struct Plane1dDecLut {
-  uint16_t e[4 * 8 * 256];  // [n][c][s]: nibble | used << 4 | n' << 8
+  uint16_t e[4 * 8 * 256];  // [n][c][s]: nibble | used << 4 | n' << 12 (n' in place for the next index)
 };
 constexpr Plane1dDecLut make_plane1d_dec_lut() {
   Plane1dDecLut t{};
@@ -995,7 +995,7 @@ constexpr Plane1dDecLut make_plane1d_dec_lut() {
         uint32_t n = n0, x = 0, used = 0;
         plane_decode_1d(s, c, n, x, used);
         n = n < 3 ? n : 3;
-        t.e[(n0 * 8 + c) * 256 + s] = (uint16_t)(x | (used << 4) | (n << 8));
+        t.e[(n0 * 8 + c) * 256 + s] = (uint16_t)(x | (used << 4) | (n << 12));
       }
   return t;
 }
@@ -1766,12 +1766,12 @@ ZFP_HD void decode_planes_1d(planes<UInt, 1>& P, uint32_t& n12, Reader& rd) {
   if constexpr (C >= 0) {
     if constexpr (C & 1)
       if (!any_lane(rd.pos < rd.end)) return;
-    const uint32_t s = rd.bits8();
+    // (c << 9 | n12: one v_lshl_or_b32, s << 1 | that: another)
     const uint32_t c = umin(rd.end - rd.pos, 7u);
-    const uint32_t e = rd.dec1d(n12 | (c << 9) | (s << 1));
+    const uint32_t e = rd.dec1d((rd.bits8() << 1) | ((c << 9) | n12));
     P.template set<H>(C, e & 15u);
     rd.pos += (e >> 4) & 15u;
-    n12 = (e << 4) & 0x3000u;
+    n12 = e & 0x3000u;
     decode_planes_1d<H, C - 1>(P, n12, rd);
   }
 }
