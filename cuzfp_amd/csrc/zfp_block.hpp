@@ -1018,7 +1018,7 @@ ZFP_HD bool encode_pairs_1d(const planes<UInt, 1>& P, uint32_t& n10, Writer& wr)
     const uint32_t a = (P.template word<H>(C) >> S) & 15u, b = (P.template word<H>(C - 1) >> S) & 15u;
     const uint32_t e = wr.pair1d(pair1d_off(n10, a, b));
     wr.put(e & 0x3fffu, (e >> 14) & 31u);
-    n10 = (e >> 20) & 0xc00u;
+    n10 = e >> 20;  // bits 19-29 of an entry are zero
     return encode_pairs_1d<H, C - 2>(P, n10, wr);
   }
   return true;
@@ -1913,6 +1913,10 @@ __device__ __forceinline__ float absmax_nan(const float* f) {
 template <int N>
 __device__ __forceinline__ void quantize_f32(const float* f, float s, bool fast, uint32_t* q) {
   typedef float f2 __attribute__((ext_vector_type(2)));
+  // 1D/2D: one path for the whole wave (the exact one is right for every
+  // block): a per-lane choice is if-converted for these small blocks, i.e.
+  // both paths run.  (3D keeps the per-lane branch the compiler lays out.)
+  if constexpr (N <= 16) fast = !any_lane(!fast);
   if (fast) {
     const f2 ss = {s, s};
 #pragma unroll
