@@ -1336,8 +1336,9 @@ ZFP_HD PW merge_at(uint32_t s, uint64_t ones, uint64_t w) {
     return (PW)bfi_v((uint32_t)hi, (uint32_t)o, (uint32_t)w) |
            ((PW)bfi_v((uint32_t)(hi >> 32), (uint32_t)(o >> 32), (uint32_t)(w >> 32)) << 32);
   } else {
-    // 16-bit planes (2D: s <= 15, ones below bit 16 - s): 32-bit shifts
-    return (PW)bfi_v(~0u << s, (uint32_t)ones << s, (uint32_t)w);
+    // 16-bit planes (2D: s <= 15, ones below bit 16 - s): the low s bits of w
+    // (one v_bfe_u32) under the shifted ones (one v_lshl_or_b32)
+    return (PW)(((uint32_t)ones << s) | low_bits((uint32_t)w, s));
   }
 }
 
@@ -1546,70 +1547,9 @@ ZFP_HD PW decode_plane_lut(unsigned& bits, unsigned& n, Reader& rd, bool& slow) 
   return lut_finish<DIMS, PW>(bits, n, rd, slow, nf, m, w, e1, e2);
 }
 
-// The decoder's plane step.  The reader holds the block's budget as an end
-// position (rd.end: the read position never passes it), so the common path
-// clips its advance with one min and keeps no separate bit count; the rare
-// paths compute the budget left as rd.end - rd.pos.  n is kept at most N-1
-// (with n = N-1 the group part is the last position's bit alone, looked up in
-// two dedicated entries, which reads the same bits as n = N), so the window
-// offset and the verbatim mask take n as it is.  Common case: the code ends
-// within the two chunks, below position N-1 (one wave-uniform test covers
-// both).
-template <int DIMS, typename PW, typename Reader>
-ZFP_HD PW decode_plane_fast(unsigned& n, Reader& rd, bool& slow, bool& rare) {
-  constexpr unsigned N = 1u << (2 * DIMS);
-  const unsigned nf = n;  // <= N-1
-  uint64_t w;
-  uint32_t g;
-  rd.windows(nf, w, g);
-  uint32_t e1, e2;
-  if constexpr (DIMS == 1) {
-    e1 = rd.chunk1_fast(g);  // a 1D code fits chunk 1
-    e2 = 0;
-  } else {
-    uint32_t e2a, e2b;
-    rd.chunks_fast(g, e1, e2a, e2b);
-    // the exit state (bit 31) as a mask by one arithmetic shift, the select
-    // by v_bfi (a compare and a v_cndmask otherwise: two slow-issue VALU ops)
-    e2 = keep_if_bit13(bfi_v((uint32_t)((int32_t)e1 >> 31), e2b, e2a), e1);
-  }
-  const uint32_t S = e1 + e2;
-  const uint32_t npos = S >> kPosShift & 31u;
-  const uint32_t used = S & kUsedMask;
-  const uint32_t ones = ((e1 >> kOnesShift) & kChunkMask) |
-                        (((e2 >> kOnesShift) & kChunkMask) << ((e1 >> kPosShift) & 31u));
-  // One wave-uniform test for both rare cases: a code longer than the two
-  // chunks (the sum carries the marker) and one reaching position N-1
-  // (nf + npos >= N; nf + npos < 2N).
-  slow = false;
-  rare = any_lane(and_or(S, kNotEnded, nf + npos) >= N);  // (nf + npos < 2N)
-  // The budget: past its budget a block reads as zeros (it ends there), so a code that ended did so within the
-  // budget or with the zero group test that follows a one read with the
-  // budget's last bit: taken as read, min(used, bits - nf) bits.  A lane with
-  // fewer than nf bits reads zeros for the rest of its verbatim part and a
-  // "0" leading test past its block: a verbatim-only plane, all its bits.  So
-  // the common path only clips the advance at the budget.  A code that did
-  // not end within the two chunks (cut by the budget, or longer than the
-  // chunks) or reaches position N-1 takes, for the whole wave, the
-  // budget-aware resolution from the entries already read (lut_finish);
-  // `slow` is left only for the general decoder's cases.
-  if (__builtin_expect(rare, 0)) {
-    unsigned bits = rd.end - rd.pos;
-    const PW x = lut_finish<DIMS, PW>(bits, n, rd, slow, nf, umin(nf, bits), w, e1, e2);
-    n = umin(n, N - 1);
-    return x;
-  }
-  // bits >= nf of the plane from the group code, below it verbatim: one
-  // v_bfi_b32 a dword under the mask ~0 << nf
-  const PW x = merge_at<PW>(nf, ones, w);
-  n = nf + npos;
-  rd.pos = umin(rd.pos + nf + used, rd.end);
-  return x;
-}
-
 // Plane loop: the table decoder for every lane, then, only when some lane of
 // the wave needs it, the general decoder for those lanes.  (n <= N-1 in and
-// out.)
+// out.)  Used for a rolled loop's trailing odd plane.
 template <int DIMS, typename PW, typename Reader>
 ZFP_HD PW decode_plane_any(unsigned& n, Reader& rd) {
   constexpr unsigned N = 1u << (2 * DIMS);
@@ -1631,30 +1571,76 @@ ZFP_HD PW decode_plane_any(unsigned& n, Reader& rd) {
   return x;
 }
 
-// Every dimensionality (1D reads chunk 1 only).  CUZFP_FAST_DIMS=2/3: the
-// budget-aware step below that (A/B builds).
-#ifndef CUZFP_FAST_DIMS
-#define CUZFP_FAST_DIMS 1
-#endif
-// The fast step with the general decoder for the lanes the tables cannot finish
-// (none on the bench fields: tools/dec_paths.cpp).
+// The decoder's plane step, every dimensionality (1D reads chunk 1 only).
+// The reader holds the block's budget as an end position (rd.end: the read
+// position never passes it), so the common path clips its advance with one
+// min and keeps no separate bit count; the rare paths compute the budget left
+// as rd.end - rd.pos.  n is kept at most N-1 (with n = N-1 the group part is
+// the last position's bit alone, looked up in two dedicated entries, which
+// reads the same bits as n = N), so the window offset and the verbatim mask
+// take n as it is.  Common case: the code ends within the two chunks, below
+// position N-1 (one wave-uniform test covers both).
 template <int DIMS, typename PW, typename Reader>
 ZFP_HD PW decode_plane_fast_any(unsigned& n, Reader& rd) {
   constexpr unsigned N = 1u << (2 * DIMS);
-  const auto pos0 = rd.pos;
-  const unsigned n0 = n;
-  bool slow, rare;
-  PW x = decode_plane_fast<DIMS, PW>(n, rd, slow, rare);
-  ZFP_COUNT_PATH(slow ? 2 : rare ? 1 : 0);
-  if (__builtin_expect(rare, 0) && any_lane(slow)) {
-    if (slow) {
-      rd.init(pos0);
-      n = n0;
-      unsigned bits = rd.end - pos0;
-      x = decode_plane<DIMS, PW>(bits, n, rd);
-      n = umin(n, N - 1);
-    }
+  const unsigned nf = n;  // <= N-1
+  uint64_t w;
+  uint32_t g;
+  rd.windows(nf, w, g);
+  uint32_t e1, e2;
+  if constexpr (DIMS == 1) {
+    e1 = rd.chunk1_fast(g);  // a 1D code fits chunk 1
+    e2 = 0;
+  } else {
+    uint32_t e2a, e2b;
+    rd.chunks_fast(g, e1, e2a, e2b);
+    // the exit state (bit 31) as a mask by one arithmetic shift, the select
+    // by v_bfi (a compare and a v_cndmask otherwise: two slow-issue VALU ops)
+    e2 = keep_if_bit13(bfi_v((uint32_t)((int32_t)e1 >> 31), e2b, e2a), e1);
   }
+  const uint32_t S = e1 + e2;
+  const uint32_t npos = S >> kPosShift & 31u;
+  const uint32_t used = S & kUsedMask;
+  // One wave-uniform test for both rare cases: a code longer than the two
+  // chunks (the sum carries the marker) and one reaching position N-1
+  // (nf + npos >= N; nf + npos < 2N).
+  if (__builtin_expect(any_lane(and_or(S, kNotEnded, nf + npos) >= N), 0)) {
+    // The budget-aware resolution from the entries already read
+    // (lut_finish) for the whole wave, and for the lanes it cannot finish
+    // (none on the bench fields: tools/dec_paths.cpp) the general decoder.
+    // Everything rare stays in this one branch, so the common path carries
+    // no flag from it.
+    const auto pos0 = rd.pos;
+    unsigned bits = rd.end - rd.pos;
+    bool slow;
+    PW x = lut_finish<DIMS, PW>(bits, n, rd, slow, nf, umin(nf, bits), w, e1, e2);
+    n = umin(n, N - 1);
+    ZFP_COUNT_PATH(slow ? 2 : 1);
+    if (any_lane(slow)) {
+      if (slow) {
+        rd.init(pos0);
+        n = nf;
+        bits = rd.end - pos0;
+        x = decode_plane<DIMS, PW>(bits, n, rd);
+        n = umin(n, N - 1);
+      }
+    }
+    return x;
+  }
+  ZFP_COUNT_PATH(0);
+  // The budget: past its budget a block reads as zeros (it ends there), so a
+  // code that ended did so within the budget or with the zero group test that
+  // follows a one read with the budget's last bit: taken as read, min(used,
+  // bits - nf) bits.  A lane with fewer than nf bits reads zeros for the rest
+  // of its verbatim part and a "0" leading test past its block: a
+  // verbatim-only plane, all its bits.  So the common path only clips the
+  // advance at the budget.
+  const uint32_t ones = ((e1 >> kOnesShift) & kChunkMask) |
+                        (((e2 >> kOnesShift) & kChunkMask) << ((e1 >> kPosShift) & 31u));
+  // bits >= nf of the plane from the group code, below it verbatim
+  const PW x = merge_at<PW>(nf, ones, w);
+  n = nf + npos;
+  rd.pos = umin(rd.pos + nf + used, rd.end);
   return x;
 }
 
@@ -1670,14 +1656,9 @@ ZFP_HD int decode_half(planes<UInt, DIMS>& P, unsigned& n, int cmin, Reader& rd)
     if constexpr (prio_of<Reader>::value)
       progress_priority<CUZFP_DPRIO_T2, CUZFP_DPRIO_T1, CUZFP_DPRIO_T0>(uniform(c));
     PW xa, xb;
-    if constexpr (DIMS >= CUZFP_FAST_DIMS) {
-      xa = decode_plane_fast_any<DIMS, PW>(n, rd);
-      xb = decode_plane_fast_any<DIMS, PW>(n, rd);
-      ZFP_STAMP(4);  // diagnostic builds: the last fast pair's end
-    } else {
-      xa = decode_plane_any<DIMS, PW>(n, rd);
-      xb = decode_plane_any<DIMS, PW>(n, rd);
-    }
+    xa = decode_plane_fast_any<DIMS, PW>(n, rd);
+    xb = decode_plane_fast_any<DIMS, PW>(n, rd);
+    ZFP_STAMP(4);  // diagnostic builds: the last fast pair's end
     const int u = uniform(c);
     P.template set<H>(u, xa);
     P.template set<H>(u - 1, xb);

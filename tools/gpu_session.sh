@@ -69,6 +69,11 @@ for s in $STEPS; do
           python tools/kernel_probe.py ${PROBE_ARGS:-} > /dev/null 2>&1
         ok_or_stop $? counters_g$i
       done ;;
+    icache)
+      # instruction-cache behaviour of the codec kernels (one --pmc pass, SQ block)
+      timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH SQC_ICACHE_INPUT_VALID_READYB SQ_WAVES SQ_BUSY_CYCLES --output-format csv -d "$OUT/ic_$TAG" -o run -- \
+        python tools/kernel_probe.py ${PROBE_ARGS:-} > /dev/null 2>&1
+      ok_or_stop $? icache ;;
     configs)
       # the other BASELINE configs: 2D f32 8192^2 rate 2, 1D f32 1M rate 8 (and 1D 64M)
       timeout -k 10 300 python bench.py --dims 2 --size 8192 --rate 2 --no-cpu-baseline --no-host-path > "$OUT/bench_2d_$TAG.json" 2>&1

@@ -21,10 +21,10 @@ OUT = os.path.join(ROOT, "build", "probe")
 VARIANTS = (0, 1, 2, 9)
 
 
-def build():
+def build(variants=VARIANTS):
     from cuzfp_amd import build as b
     procs = []
-    for v in VARIANTS:
+    for v in variants:
         d = os.path.join(OUT, f"p{v}")
         os.makedirs(d, exist_ok=True)
         objs = []
@@ -33,8 +33,14 @@ def build():
             objs.append(o)
             procs.append(subprocess.Popen([b.HIPCC, *b.CXXFLAGS, f"-DCUZFP_PROBE={v}", "-c",
                                            os.path.join(b.CSRC, u + ".hip"), "-o", o]))
-    assert all(p.wait() == 0 for p in procs)
-    for v in VARIANTS:
+    import time
+    t0 = time.time()
+    while any(p.poll() is None for p in procs):  # a heartbeat line for long builds
+        time.sleep(2)
+        if int(time.time() - t0) % 30 < 2:
+            print(f"building ... {int(time.time() - t0)} s", flush=True)
+    assert all(p.returncode == 0 for p in procs)
+    for v in variants:
         d = os.path.join(OUT, f"p{v}")
         objs = [os.path.join(d, u + ".o") for u in ("inst_f32", "inst_f64", "inst_i32", "inst_i64", "capi")]
         subprocess.check_call([b.HIPCC, f"--offload-arch={b.ARCH}", "-shared", "-fPIC", "-o",
@@ -155,11 +161,12 @@ if __name__ == "__main__":
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--field", default="polynomial")
     ap.add_argument("--back", type=int, default=1, help="stamped launches back to back (the last one's stamps)")
+    ap.add_argument("--variants", default=",".join(map(str, VARIANTS)), help="build: CUZFP_PROBE values")
     ap.add_argument("--dims", type=int, default=3)
     ap.add_argument("--rate", type=float, default=8.0)
     a = ap.parse_args()
     if a.cmd == "build":
-        build()
+        build(tuple(int(v) for v in a.variants.split(",")))
     elif a.cmd == "stamps":
         od = os.path.join(ROOT, "gpurun_out")
         os.makedirs(od, exist_ok=True)
