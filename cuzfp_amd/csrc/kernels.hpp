@@ -390,16 +390,49 @@ struct LdsReader {
 // < 16), so a window is one 64-bit shift of the zero-extended block, without
 // the bounds test and selects a block of up to 64 bits needs (five of the
 // plane step's slow-issue VALU instructions).
+// B32 also keeps the block shifted up by 2 (blk4): the group window is taken
+// from it, so a chunk's 10 bits sit at bits 2-11, already a byte offset of
+// the 4-byte entries (one AND instead of a shift and an AND).
 template <bool PRIO = true, bool B32 = false>
 struct RegReader : LdsReader<PRIO> {
-  uint64_t blk;
+  uint64_t blk, blk4;
+  __device__ __forceinline__ void set_block(uint64_t b) {
+    blk = b;
+    if constexpr (B32) blk4 = b << 2;
+  }
   __device__ __forceinline__ uint64_t at(uint32_t p) const {
     if constexpr (B32) return blk >> p;
     return p < 64 ? blk >> p : 0ull;
   }
   __device__ __forceinline__ void windows(uint32_t m, uint64_t& w, uint32_t& g) const {
     w = at(this->pos);
-    g = (uint32_t)at(this->pos + m);
+    if constexpr (B32)
+      g = (uint32_t)(blk4 >> (this->pos + m));  // the group window << 2
+    else
+      g = (uint32_t)at(this->pos + m);
+  }
+  // (B32: g from windows() is the group window << 2; its bit 2 is the leading
+  // test)
+  __device__ __forceinline__ void chunks_fast(uint32_t g, uint32_t& e1, uint32_t& e2a, uint32_t& e2b) const {
+    if constexpr (B32) {
+      // (no lead mask here: at 8 waves a SIMD the 2D decoder's LDS is not
+      // what it waits on, and the mask's two VALU a plane are)
+      e1 = this->tab(g & 0xffcu);
+      const uint2 p = this->tab64(LdsReader<PRIO>::kPairBytes + ((g >> 9) & 0x1ff8u));
+      e2a = p.x;
+      e2b = p.y;
+    } else {
+      LdsReader<PRIO>::chunks_fast(g, e1, e2a, e2b);
+    }
+  }
+  __device__ __forceinline__ uint32_t chunk1_fast(uint32_t g) const {
+    if constexpr (B32) {
+      uint32_t t;
+      asm("v_bfe_i32 %0, %1, 2, 1" : "=v"(t) : "v"(g));
+      return this->tab((g & t) & 0xffcu);
+    } else {
+      return LdsReader<PRIO>::chunk1_fast(g);
+    }
   }
   __device__ __forceinline__ uint64_t peek() const { return at(this->pos); }
   __device__ __forceinline__ uint32_t window32(uint32_t q) const { return (uint32_t)at(q); }
@@ -925,7 +958,7 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) voi
       rd.lds32 = L;
       rd.lut32 = lut;
       rd.d1d = dtab;
-      rd.blk = blk;
+      rd.set_block(blk);
       rd.init(0);
       coded = decode_block<Scalar, DIMS>(f, g.maxbits, rd);
     } else {
@@ -1067,7 +1100,7 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) voi
       rd.lds32 = nullptr;
       rd.lut32 = ctab;
       rd.d1d = dtab;
-      rd.blk = blk;
+      rd.set_block(blk);
       rd.init(0);
       const bool coded = decode_block<Scalar, DIMS>(f, g.maxbits, rd);
       if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);
