@@ -289,17 +289,10 @@ struct LdsReader {
   __device__ __forceinline__ uint32_t tab(uint32_t byte_off) const {
     return *(lds_u32*)((uintptr_t)(lds_u32*)lut32 + byte_off);
   }
-  // g with every bit cleared unless its leading group test (bit 0) is 1: a
-  // lane whose test reads "0" (no new ones: about half the lane-steps) looks
-  // up entry 0 for both chunks -- the same "0" entry as any even chunk, and a
-  // chunk 2 that is dropped anyway -- so those lanes' reads are broadcasts
-  // instead of bank conflicts (random entries made 51 % of the decoder's LDS
-  // cycles conflict cycles, SQ_LDS_BANK_CONFLICT)
-  static __device__ __forceinline__ uint32_t lead_masked(uint32_t g) {
-    uint32_t t;
-    asm("v_bfe_i32 %0, %1, 0, 1" : "=v"(t) : "v"(g));
-    return g & t;
-  }
+  // (The chunk lookups index the tables with the window as read.  Masking it
+  // to zero for lanes whose leading test is "0" -- entry 0, a broadcast --
+  // cut the LDS bank-conflict cycles, but its two VALU a plane cost more:
+  // 256^3 r8 decode 23.5 -> 23.2 us without it, tools/xvar.py, r04_nolead.)
   // byte offsets of chunk 1's state-2 entry (chunk bits 0-9; the state-2
   // table is at LDS address 0) and of chunk 2's pair of state-0/1 entries
   // (bits 10-19; from the pair table's start, kLutPairs)
@@ -324,9 +317,8 @@ struct LdsReader {
   // position's bit alone; the parse then runs past position N-1, which the
   // steps' implied-one rule resolves.)
   __device__ __forceinline__ void chunks_fast(uint32_t g, uint32_t& e1, uint32_t& e2a, uint32_t& e2b) const {
-    const uint32_t gm = lead_masked(g);
-    e1 = tab(off1(gm));
-    const uint2 p = tab64(kPairBytes + off2(gm));
+    e1 = tab(off1(g));
+    const uint2 p = tab64(kPairBytes + off2(g));
     e2a = p.x;
     e2b = p.y;
   }
@@ -344,7 +336,7 @@ struct LdsReader {
     eBb = p.y;
   }
   __device__ __forceinline__ uint32_t chunk1_fast(uint32_t g) const {
-    return tab(off1(lead_masked(g)));
+    return tab(off1(g));
   }
   // 1D: an entry of the plane table (o: byte offset) and the 8 stream bits at pos
   typedef __attribute__((address_space(3))) const uint16_t lds_u16;
