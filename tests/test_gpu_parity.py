@@ -383,6 +383,41 @@ def test_int_register_writer(cuda, restatement, dims, dtype, mb):
             assert np.array_equal(y, restatement.decompress(ref, shape, dtype, mb)), (shape, kind)
 
 
+@pytest.mark.parametrize("dims", [1, 2])
+def test_register_writer_extremes(cuda, restatement, dims):
+    """f32 blocks of 32 bits (1D rate 8, 2D rate 2: RegWriter32, which keeps
+    stream bits 1..32 and relies on a coded block's first bit being one) and
+    of 64 bits, on blocks that take every quantisation path: all-zero blocks
+    (no exponent field), denormals and tiny exponents (the exact path, for the
+    whole wave), huge values, inf and NaN, mixed with smooth blocks in the
+    same waves; 1D also past 32,768 waves (the batched kernels)."""
+    rng = np.random.default_rng(55 + dims)
+    shapes = [(4 * 64 * 7 + 3,), (4 * 64 * 32769 + 2,)] if dims == 1 else [(90, 75), (260, 514)]
+    for shape in shapes:
+        a = _fields(rng, shape, np.float32, "smooth")
+        flat = a.reshape(-1)
+        n = flat.size
+        idx = rng.permutation(n)
+        k = n // 16
+        flat[idx[:k]] = 0.0
+        flat[idx[k:2 * k]] *= np.float32(1e-38)
+        flat[idx[2 * k:3 * k]] = (rng.standard_normal(k) * 1e-44).astype(np.float32)
+        with np.errstate(over="ignore"):
+            flat[idx[3 * k:4 * k]] *= np.float32(3e37)
+        flat[idx[4 * k:4 * k + 50]] = np.inf
+        flat[idx[4 * k + 50:4 * k + 100]] = -np.inf
+        flat[idx[4 * k + 100:4 * k + 150]] = np.nan
+        if dims == 1:
+            flat[: 4 * 64] = 0.0  # a whole wave of zero blocks
+        else:
+            a[:8, :] = 0.0
+        for mb in (32, 64):
+            words, y = _gpu_roundtrip(a, mb, cuda)
+            ref = restatement.compress(a, mb)
+            assert np.array_equal(words, ref), (shape, mb)
+            assert np.array_equal(y.view(np.uint8), restatement.decompress(ref, shape, np.float32, mb).view(np.uint8)), (shape, mb)
+
+
 @pytest.mark.parametrize("nblocks", [64 * 32771, 64 * 32769 + 25, 64 * 32768 - 1])
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 def test_batched_1d_waves(cuda, restatement, nblocks, dtype):
