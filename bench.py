@@ -638,13 +638,20 @@ def main():
     # reference's (N=1; the timed steps rewrote the same words), configs[4]'s parity
     parity = None
     gpath = os.path.join(ROOT, "tests", "golden", "golden.json")
-    key = {("float32", 8.0): "baseline/3d_f32_256_r8", ("float64", 16.0): "baseline/3d_f64_256_r16"}.get(
-        (args.dtype, args.rate))
-    if key and dims == 3 and n == 256 and world == 1 and not strong and os.path.exists(gpath):
+    key = {(3, 256, "float32", 8.0): "baseline/3d_f32_256_r8", (3, 256, "float64", 16.0): "baseline/3d_f64_256_r16",
+           (2, 8192, "float32", 2.0): "baseline/2d_f32_8192_r2",
+           (1, 1048576, "float32", 8.0): "baseline/1d_f32_1M_r8"}.get((dims, n, args.dtype, float(args.rate)))
+    if key and world == 1 and not strong and os.path.exists(gpath):
         rec = json.load(open(gpath))["cases"].get(f"{key}/{args.field}")
         if rec:
             got = hashlib.sha256(words.cpu().numpy().tobytes()).hexdigest()
-            parity = "stream sha256 == reference zfp 0.5.0" if got == rec["stream_sha256"] else "MISMATCH"
+            dec = hashlib.sha256(y.cpu().numpy().tobytes()).hexdigest()
+            if got != rec["stream_sha256"]:
+                parity = "MISMATCH (stream)"
+            elif dec != rec.get("decoded_sha256", dec):
+                parity = "MISMATCH (decoded array)"
+            else:
+                parity = "stream and decoded sha256 == reference zfp 0.5.0"
     config5 = None
     if c5 is not None:
         config5 = c5 if "error" in c5 else finish_config5(c5, world, rank, dev, dist)
