@@ -42,6 +42,7 @@ static int make_problem(int type, unsigned nx, unsigned ny, unsigned nz, long lo
   g.maxbits = maxbits;
   g.wave0 = 0;
   g.vec_io = 0;
+  g.row_stage = 0;
   g.sx = sx ? sx : 1;
   g.sy = sy ? sy : (long long)g.nx;
   g.sz = sz ? sz : (long long)g.nx * g.ny;

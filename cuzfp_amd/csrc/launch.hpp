@@ -25,6 +25,9 @@ struct Geometry {
   // n < 2^31 (set_divisor), by bx and by bx * by; divmagic = 0 when nblocks
   // is too large for it (plain division then)
   uint32_t dbx_m, dbx_s, dpl_m, dpl_s, divmagic;
+  // 3D double decoder: rows a pass when its row stores are staged through the
+  // wave's LDS image (0: stored straight from the lanes), see kernels.hpp
+  uint32_t row_stage;
 };
 
 // q = floor(n / d) = (n * m) >> s for every n < 2^31, with s = 31 + ceil(log2 d)

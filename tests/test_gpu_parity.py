@@ -418,6 +418,23 @@ def test_register_writer_extremes(cuda, restatement, dims):
             assert np.array_equal(y.view(np.uint8), restatement.decompress(ref, shape, np.float32, mb).view(np.uint8)), (shape, mb)
 
 
+def test_f64_staged_rows(cuda, restatement):
+    """3D double decodes whose waves are whole x-row segments (256 wide: 64
+    blocks) store their rows through the wave's LDS image (kernels.hpp,
+    scatter_f64_staged: 4, 2 or 1 rows a pass by maxbits, none below), with
+    zero blocks among coded ones in the same waves."""
+    rng = np.random.default_rng(64)
+    a = _fields(rng, (8, 12, 256), np.float64, "smooth")
+    a[:, :4, :64] = 0.0      # zero blocks in a wave's first half
+    a[4:, 4:8, 192:] = 0.0   # ... and in its last quarter
+    for rate in (16, 8, 2, 1, 40):
+        mb = cz.rate_to_maxbits(rate, np.float64, 3)
+        words, y = _gpu_roundtrip(a, mb, cuda)
+        ref = restatement.compress(a, mb)
+        assert np.array_equal(words, ref), rate
+        assert np.array_equal(y.view(np.uint8), restatement.decompress(ref, a.shape, np.float64, mb).view(np.uint8)), rate
+
+
 @pytest.mark.parametrize("nblocks", [64 * 32771, 64 * 32769 + 25, 64 * 32768 - 1])
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 def test_batched_1d_waves(cuda, restatement, nblocks, dtype):
