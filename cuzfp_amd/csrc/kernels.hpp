@@ -801,6 +801,9 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS, true>::value
   // W words per block plus kSlackWords rows
   const uint32_t W = g.maxbits >> 6;
   Scalar f[N];
+  // (3D double rows staged through LDS like the decoder's stores
+  // (gather_f64_staged, round 4) measured slower: 256^3 r16 encode 51.1 ->
+  // 54.5 us, the passes' LDS round trips sitting on the loads' critical path)
   if (b < g.nblocks) gather<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
   // (one copy a workgroup behind a barrier measured slower: 28.0 -> 28.4 us at 256^3)
   if constexpr (!kGroupSpread) {
@@ -1296,6 +1299,7 @@ int launch_encode_t(const void* data, const Geometry& g, bool fast, uint64_t* st
   // (whose padded image would pass the workgroup's LDS) take the general writer
   const bool aligned = (g.maxbits & 63) == 0 && gg.lds_words * 8 + kStatic <= lds_cap_bytes();
   if (!aligned) gg.lds_words = g.maxbits + 2;
+  gg.row_stage = 0;  // (the decoder's staged row stores only)
   // one wave's image beside the tables must fit the workgroup's LDS budget
   if (gg.lds_words * 8 + kStatic > lds_cap_bytes()) return CUZFP_ERROR_INVALID_ARGUMENT;
   const uint32_t wpg = waves_per_group(gg.lds_words, kStatic, kEncWaves);
