@@ -801,9 +801,10 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS, true>::value
   // W words per block plus kSlackWords rows
   const uint32_t W = g.maxbits >> 6;
   Scalar f[N];
-  // (3D double rows staged through LDS like the decoder's stores
-  // (gather_f64_staged, round 4) measured slower: 256^3 r16 encode 51.1 ->
-  // 54.5 us, the passes' LDS round trips sitting on the loads' critical path)
+  // (3D double rows staged through LDS like the decoder's stores measured
+  // slower, round 4: 256^3 r16 encode 51.1 -> 54.5 us with non-temporal
+  // loads, 50.9 -> 54.4 us with plain ones; non-temporal hints on these
+  // strided row loads: 50.9 -> 55.6 us)
   if (b < g.nblocks) gather<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
   // (one copy a workgroup behind a barrier measured slower: 28.0 -> 28.4 us at 256^3)
   if constexpr (!kGroupSpread) {
