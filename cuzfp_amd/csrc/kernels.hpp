@@ -849,6 +849,35 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS, true>::value
   const uint32_t nwords = (nb * g.maxbits + 63) >> 6;
   uint64_t* out = stream + (size_t)wave * g.maxbits;
   if constexpr (ALIGNED) {
+    if (nb == kLanes && g.vec_io && !(W & 1)) {
+      // A full wave stores its 64 W words in lane order, each store covering
+      // 1 KiB contiguously (non-temporal): store t covers words [128 t, 128 t
+      // + 128), lane l's two at k = 128 t + 2 l, words j = k % W, j + 1 of
+      // block s = k / W (column s of the image).  Each lane storing its own
+      // W words instead puts every store instruction's 16-byte pieces W * 8
+      // bytes apart: 256^3 r8 encode 27.4 -> 24.4 us, step 50.3 -> 49.2 us;
+      // 1024^3 step -0.5 % (tools/xvar.py, r04_stream_stores; plain stores
+      // here gave encode 26.5 us and a faster decode of the still-cached
+      // stream at 256^3, step 48.8 us, but a cached stream is the bench's
+      // artefact, not a decompressor's).
+      uint32_t s = (2 * lane) / W, j = (2 * lane) % W;
+      const uint32_t ds = 128 / W, dj = 128 % W;
+      for (uint32_t k = 2 * lane; k < kLanes * W; k += 128) {
+        uint4 v;
+        const uint64_t a0 = lds[j * 64 + s], a1 = lds[(j + 1) * 64 + s];
+        __builtin_memcpy(&v.x, &a0, 8);
+        __builtin_memcpy(&v.z, &a1, 8);
+        st16<true>(&out[k], v);
+        j += dj;
+        s += ds;
+        if (j >= W) { j -= W; s++; }
+      }
+      ZFP_STAMP(6);
+      ZFP_STAMP_REAL(9);
+      return;
+    }
+  }
+  if constexpr (ALIGNED) {
     // each lane stores its own block: W words at out + lane * W
     if (b < g.nblocks) {
       const uint64_t* mine = lds + lane;
@@ -941,7 +970,20 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) voi
     const bool vec = (g.maxbits & 127) == 0 && g.vec_io;
     constexpr uint32_t kHeld = 8;  // 16-byte pieces held in registers (maxbits <= 1024)
     uint4 held[kHeld];
-    if (live && vec) {
+    // A full wave loads its segment in lane order, each load 1 KiB
+    // contiguously with the non-temporal hint, and places the pieces in the
+    // lanes' columns (the same LDS writes at other addresses).  Lane-owned
+    // loads put each instruction's pieces D * 4 bytes apart.  256^3 r8
+    // (tools/xvar.py, r04_stream_loads): step 48.9 -> 48.2 us (polynomial),
+    // 46.2 -> 45.1 (splitmix); the decoder alone, replayed on one cached
+    // stream, 23.4 -> 24.9 us (plain contiguous loads: unchanged).
+    const bool cont = vec && wave < g.wave_end && g.nblocks - wave * kLanes >= kLanes && D <= 4 * kHeld;
+    if (cont) {
+      const uint4* src = (const uint4*)seg + lane;
+#pragma unroll
+      for (uint32_t q = 0; q < kHeld; q++)
+        if (4 * q < D) held[q] = ld16<true>(&src[64 * q]);
+    } else if (live && vec) {
       const uint4* src = (const uint4*)(seg + lane * D);
 #pragma unroll
       for (uint32_t q = 0; q < kHeld; q++)
@@ -950,7 +992,23 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) voi
     for (uint32_t i = threadIdx.x; i < kLutEnd; i += blockDim.x)
       ((uint4*)lut)[i] = ((const uint4*)g_chunk_lut.e)[i];
     copy_dtab();
-    if (live) {
+    if (cont) {
+      // piece 64 q + lane: dwords j .. j + 3 of block s, 4 (64 q + lane) = s D + j
+      uint32_t* L0 = (uint32_t*)lds;
+      uint32_t sb = (4 * lane) / D, j = (4 * lane) % D;
+      const uint32_t dsb = 256 / D, dj = 256 % D;
+#pragma unroll
+      for (uint32_t q = 0; q < kHeld; q++)
+        if (4 * q < D) {
+          L0[(j) * 64 + sb] = held[q].x;
+          L0[(j + 1) * 64 + sb] = held[q].y;
+          L0[(j + 2) * 64 + sb] = held[q].z;
+          L0[(j + 3) * 64 + sb] = held[q].w;
+          j += dj;
+          sb += dsb;
+          if (j >= D) { j -= D; sb++; }
+        }
+    } else if (live) {
       if (vec) {
 #pragma unroll
         for (uint32_t q = 0; q < kHeld; q++)
