@@ -977,6 +977,8 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) voi
     // (tools/xvar.py, r04_stream_loads): step 48.9 -> 48.2 us (polynomial),
     // 46.2 -> 45.1 (splitmix); the decoder alone, replayed on one cached
     // stream, 23.4 -> 24.9 us (plain contiguous loads: unchanged).
+    // (1024^3 r8, the same session: the step within +-0.5 % for contiguous
+    // non-temporal, contiguous plain and lane-owned loads, r04_stream_loads)
     const bool cont = vec && wave < g.wave_end && g.nblocks - wave * kLanes >= kLanes && D <= 4 * kHeld;
     if (cont) {
       const uint4* src = (const uint4*)seg + lane;
