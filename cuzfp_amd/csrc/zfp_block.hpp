@@ -1610,6 +1610,8 @@ ZFP_HD PW decode_plane_fast_any(unsigned& n, Reader& rd) {
     // (none on the bench fields: tools/dec_paths.cpp) the general decoder.
     // Everything rare stays in this one branch, so the common path carries
     // no flag from it.
+    // (design statistics, tools/dec_paths.cpp: why a lane is rare)
+    ZFP_COUNT_PATH((S & kNotEnded) ? 16 : (nf + npos >= N) ? 17 : 18);
     const auto pos0 = rd.pos;
     unsigned bits = rd.end - rd.pos;
     bool slow;

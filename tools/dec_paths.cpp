@@ -10,7 +10,7 @@
 #include <string.h>
 #include <vector>
 static int g_path[96], g_calls;
-static long g_reason[8];
+static long g_reason[16];
 #define ZFP_COUNT_PATH(id) \
   do { if ((id) >= 10) g_reason[(id) - 10]++; else if (g_calls < 96) g_path[g_calls++] = (id); } while (0)
 #include "../cuzfp_amd/csrc/zfp_block.hpp"
@@ -80,6 +80,8 @@ int main(int argc, char** argv) {
   for (int p = 0; p < 9; p++)
     printf("  %d %-18s lane-steps per block %6.3f   wave-steps per wave %6.3f\n", p, nm[p], lane[p] / (double)blocks,
            wave[p] / nw);
+  printf("rare lane-steps per block: code past two chunks %.4f, reaching position N-1 %.4f, neither %.4f\n",
+         g_reason[6] / (double)blocks, g_reason[7] / (double)blocks, g_reason[8] / (double)blocks);
   printf("table step outcomes per block: ok %.3f  implied+cut %.4f  implied %.4f  cut P>q %.4f  open %.4f  other %.4f\n",
          g_reason[0] / (double)blocks, g_reason[1] / (double)blocks, g_reason[2] / (double)blocks,
          g_reason[3] / (double)blocks, g_reason[4] / (double)blocks, g_reason[5] / (double)blocks);
