@@ -1449,7 +1449,11 @@ int launch_decode_t(const uint64_t* stream, const Geometry& g, bool fast, void* 
       return e == hipSuccess ? CUZFP_SUCCESS : CUZFP_ERROR_HIP;
     }
   }
-  if (fast && !use_priority(nwaves, occupancy<Scalar, DIMS>::value, 2))
+  // the decoder keeps the priority schedule up to two resident rounds; 3D
+  // double (two waves a SIMD) up to one: at 256^3 r16 (two rounds) its decode
+  // measured 56.6 -> 54.9 us without it (r04_f64prio)
+  constexpr uint32_t kDecPrioRounds = (sizeof(Scalar) == 8 && DIMS == 3) ? 1 : 2;
+  if (fast && !use_priority(nwaves, occupancy<Scalar, DIMS>::value, kDecPrioRounds))
     hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, true, false>), grid, block, lds, st, stream, gg, d);
   else if (fast)
     hipLaunchKernelGGL((zfp_decode<Scalar, DIMS, true>), grid, block, lds, st, stream, gg, d);
