@@ -18,7 +18,7 @@ static float poly(float x) {
   return x + xx * yy;
 }
 
-static long g_wide_r15 = 0, g_wide_len_only = 0;
+static long g_wide_r15 = 0, g_wide_len_only = 0, g_med24 = 0, g_med31 = 0;
 int main(int argc, char** argv) {
   const int n = argc > 1 ? atoi(argv[1]) : 256;
   const int rough = argc > 2 ? atoi(argv[2]) : 0;
@@ -40,6 +40,7 @@ int main(int argc, char** argv) {
   for (size_t w = 0; w < nwaves; w++) {
     int wsteps = 0;
     bool act[64][32] = {}, rz[64][32] = {}, wide[64][32] = {}, full[64][32] = {}, fit[64][32] = {}, r15[64][32] = {};
+    bool r24[64][32] = {}, r31[64][32] = {};
     unsigned glen[64][32] = {};
     for (int l = 0; l < 64; l++) {
       const size_t b = w * 64 + l;
@@ -75,6 +76,8 @@ int main(int argc, char** argv) {
         rz[l][k] = r == 0;
         wide[l][k] = (r >> 16) != 0;
         r15[l][k] = (r >> 15) != 0;
+        r24[l][k] = (r >> 24) != 0;
+        r31[l][k] = (r >> 31) != 0;
         full[l][k] = nn == 64;
         // plane code length (unbudgeted)
         unsigned len = nn;
@@ -109,8 +112,10 @@ int main(int argc, char** argv) {
       fprintf(wf, "%d\n", wsteps);
     }
     for (int k = 0; k < wsteps; k++) {
-      bool any15 = false, anylong = false;
-      for (int l = 0; l < 64; l++) if (act[l][k]) { any15 |= r15[l][k]; anylong |= !fit[l][k]; }
+      bool any15 = false, anylong = false, any24 = false, any31 = false;
+      for (int l = 0; l < 64; l++) if (act[l][k]) { any15 |= r15[l][k]; anylong |= !fit[l][k]; any24 |= r24[l][k]; any31 |= r31[l][k]; }
+      g_med24 += any15 && !any24 && !anylong;
+      g_med31 += any15 && !any31 && !anylong;
       g_wide_r15 += any15; g_wide_len_only += !any15 && anylong;
       bool all0 = true, anyw = false, allf = true, allfit = true;
       unsigned gmax = 0;
@@ -138,6 +143,7 @@ int main(int argc, char** argv) {
     }
   }
   printf("wide wave-steps per wave: some lane r >= 2^15 %.2f, only len > 64 %.2f\n", (double)g_wide_r15 / nwaves, (double)g_wide_len_only / nwaves);
+  printf("  of the r >= 2^15 ones, every lane r < 2^24 and len <= 64: %.2f; r < 2^31 and len <= 64: %.2f\n", (double)g_med24 / nwaves, (double)g_med31 / nwaves);
   printf("blocks %zu waves %zu: planes per block mean %.2f, wave steps mean %.2f\n", blocks, nwaves,
          (double)sum_planes / blocks, (double)sum_wave_steps / nwaves);
   printf("step lanes_act%%  r==0%%  n==64%%  r>=2^16%% | waves: steps  all_r0%%  any_wide%%  all_full%%  all_fit64%%  grp>20%% grp>40%% grp>60%%\n");

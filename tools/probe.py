@@ -91,7 +91,7 @@ os.environ['CUZFP_HIP_LIB'] = @LIB@
 import cuzfp_amd as cz
 from cuzfp_amd.datagen import polynomial_field, splitmix_uniform
 shape = @SHAPE@
-arr = polynomial_field(shape) if @FIELD@ == 'polynomial' else splitmix_uniform(shape)
+arr = polynomial_field(shape, @DTYPE@) if @FIELD@ == 'polynomial' else splitmix_uniform(shape, @DTYPE@)
 x = torch.from_numpy(arr).cuda()
 mb = cz.rate_to_maxbits(@RATE@, arr.dtype, @DIMS@)
 lib = cz.library()
@@ -101,22 +101,24 @@ out = {}
 for name, fn in (("encode", lambda: cz.encode(x, mb, out=w)), ("decode", lambda: cz.decode(w, shape, x.dtype, mb, out=y))):
     for _ in range(3): fn()
     torch.cuda.synchronize()
-    lib.cuzfp_hip_probe_clear()
+    sfx = "_f64" if @DTYPE@ == "float64" else ""  # each unit has its own stamp buffer
+    getattr(lib, "cuzfp_hip_probe_clear" + sfx)()
     # back to back, as in the bench: the second launch's stamps overwrite the first's
     for _ in range(@BACK@): fn()
     torch.cuda.synchronize()
     buf = np.zeros(65536 * 10, np.uint64)
-    lib.cuzfp_hip_probe_stamps(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes))
+    getattr(lib, "cuzfp_hip_probe_stamps" + sfx)(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes))
     np.save(os.path.join(@OUTDIR@, "stamps_" + name + "_" + @FIELD@ + "_" + str(@SIZE@) + ".npy"), buf.reshape(-1, 10)[:nw])
 print("ok")
 """
 
 
-def stamps(size, field, outdir, back=1, dims=3, rate=8.0):
+def stamps(size, field, outdir, back=1, dims=3, rate=8.0, dtype="float32"):
     lib = os.path.join(OUT, "p9", "libcuzfp_hip.so")
     code = STAMP_CODE.replace("@ROOT@", repr(ROOT)).replace("@LIB@", repr(lib)).replace("@SIZE@", str(size)) \
         .replace("@FIELD@", repr(field)).replace("@OUTDIR@", repr(outdir)).replace("@BACK@", str(back)) \
-        .replace("@SHAPE@", _shape(size, dims)).replace("@DIMS@", str(dims)).replace("@RATE@", str(rate))
+        .replace("@SHAPE@", _shape(size, dims)).replace("@DIMS@", str(dims)).replace("@RATE@", str(rate)) \
+        .replace("@DTYPE@", repr(dtype))
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     if r.returncode:
         print(r.stderr[-3000:])
@@ -164,12 +166,13 @@ if __name__ == "__main__":
     ap.add_argument("--variants", default=",".join(map(str, VARIANTS)), help="build: CUZFP_PROBE values")
     ap.add_argument("--dims", type=int, default=3)
     ap.add_argument("--rate", type=float, default=8.0)
+    ap.add_argument("--dtype", default="float32")
     a = ap.parse_args()
     if a.cmd == "build":
         build(tuple(int(v) for v in a.variants.split(",")))
     elif a.cmd == "stamps":
         od = os.path.join(ROOT, "gpurun_out")
         os.makedirs(od, exist_ok=True)
-        stamps(a.size, a.field, od, a.back, a.dims, a.rate)
+        stamps(a.size, a.field, od, a.back, a.dims, a.rate, a.dtype)
     else:
         run(a.size, a.field, a.dims, a.rate)
