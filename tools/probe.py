@@ -52,7 +52,7 @@ def _shape(size, dims):
     return "(" + ",".join([str(size)] * dims) + ",)"
 
 
-def run(size, field, dims=3, rate=8.0, reps=20):
+def run(size, field, dims=3, rate=8.0, reps=20, dtype="float32"):
     res = {}
     for v in (0, 1, 2):
         lib = os.path.join(OUT, f"p{v}", "libcuzfp_hip.so")
@@ -63,7 +63,7 @@ os.environ['CUZFP_HIP_LIB'] = {lib!r}
 import cuzfp_amd as cz
 from cuzfp_amd.datagen import polynomial_field, splitmix_uniform
 shape = {_shape(size, dims)}
-arr = polynomial_field(shape) if {field!r} == 'polynomial' else splitmix_uniform(shape)
+arr = polynomial_field(shape, {dtype!r}) if {field!r} == 'polynomial' else splitmix_uniform(shape, {dtype!r})
 x = torch.from_numpy(arr).cuda()
 mb = cz.rate_to_maxbits({rate}, arr.dtype, {dims})
 w = cz.encode(x, mb); y = cz.decode(w, shape, x.dtype, mb)
@@ -175,4 +175,4 @@ if __name__ == "__main__":
         os.makedirs(od, exist_ok=True)
         stamps(a.size, a.field, od, a.back, a.dims, a.rate, a.dtype)
     else:
-        run(a.size, a.field, a.dims, a.rate)
+        run(a.size, a.field, a.dims, a.rate, dtype=a.dtype)
