@@ -904,6 +904,11 @@ ZFP_HD bool encode_half_fixed(const planes<UInt, DIMS>& P, unsigned& n, Writer& 
   return true;
 }
 
+#ifdef CUZFP_ENC_AHEAD32
+constexpr bool kEncodeAhead32 = true;  // (timing builds: 32-bit coefficients too)
+#else
+constexpr bool kEncodeAhead32 = false;
+#endif
 #ifndef CUZFP_NO_AHEAD
 constexpr bool kEncodeAhead = true;
 #else
@@ -929,10 +934,13 @@ ZFP_HD uint32_t bitlen64(uint64_t r) {
 // is known before this plane's code is built; e0 / e1 carry the entries of
 // r's bytes 0 and 1 into the step that uses them (unused by the wide step).
 // Planes (H, C) .. (0, 0); false once the block is full (as encode_half_fixed).
-template <int H, int C, bool PRI, typename UInt, typename Writer>
+// EXACT = false (32-bit coefficients, timing builds): the next n from r's
+// low 16 bits (bitlen16, exact where the one-put step runs); after a wide step
+// the next plane's entries are read again with the n it leaves.
+template <int H, int C, bool PRI, bool EXACT = true, typename UInt, typename Writer>
 ZFP_HD bool encode_planes_ahead(const planes<UInt, 3>& P, unsigned& n, uint32_t& e0, uint32_t& e1, Writer& wr) {
   if constexpr (C < 0) {
-    if constexpr (H > 0) return encode_planes_ahead<H - 1, 31, false>(P, n, e0, e1, wr);
+    if constexpr (H > 0) return encode_planes_ahead<H - 1, 31, false, EXACT>(P, n, e0, e1, wr);
     return true;
   } else {
     if constexpr (C & 1) {  // a pair's first plane: the budget test, as encode_half_fixed
@@ -950,12 +958,13 @@ ZFP_HD bool encode_planes_ahead(const planes<UInt, 3>& P, unsigned& n, uint32_t&
     const unsigned nf = n;
     const uint64_t r = x >> nf;
     const uint32_t rl = (uint32_t)r;
-    const uint32_t bl = bitlen64(r);
+    const uint32_t bl = EXACT ? bitlen64(r) : bitlen16(rl);
     const PlaneLen pl = plane_len<3>(nf, bl, (uint32_t)__builtin_popcount(rl) + bl);
-    const unsigned nn = pl.nn - pl.imp;  // min(n + bitlen(r), 63): the next plane's n
+    unsigned nn = pl.nn - pl.imp;  // min(n + bitlen(r), 63): the next plane's n
     uint32_t f0 = 0, f1 = 0;
+    uint64_t xn = 0;
     if constexpr (C > 0 || H > 0) {
-      const uint64_t xn = C > 0 ? P.template get<H>(C > 0 ? C - 1 : 0) : P.template get<(H > 0 ? H - 1 : 0)>(31);
+      xn = C > 0 ? P.template get<H>(C > 0 ? C - 1 : 0) : P.template get<(H > 0 ? H - 1 : 0)>(31);
       const uint32_t rn = (uint32_t)(xn >> nn);
       f0 = wr.sp0(byte_off4<0>(rn));
       f1 = wr.sp1(byte_off4<1>(rn));
@@ -969,11 +978,17 @@ ZFP_HD bool encode_planes_ahead(const planes<UInt, 3>& P, unsigned& n, uint32_t&
     } else {
       unsigned nw = nf;
       encode_plane_wide(x, nw, wr);
+      if constexpr (!EXACT && (C > 0 || H > 0)) {
+        nn = nw;
+        const uint32_t rn = (uint32_t)(xn >> nn);
+        f0 = wr.sp0(byte_off4<0>(rn));
+        f1 = wr.sp1(byte_off4<1>(rn));
+      }
     }
     n = nn;
     e0 = f0;
     e1 = f1;
-    return encode_planes_ahead<H, C - 1, PRI>(P, n, e0, e1, wr);
+    return encode_planes_ahead<H, C - 1, PRI, EXACT>(P, n, e0, e1, wr);
   }
 }
 
@@ -1109,6 +1124,12 @@ ZFP_HD void encode_planes(const planes<UInt, DIMS>& P, unsigned maxprec, Writer&
     if constexpr (DIMS == 1 && has_pair1d<Writer>::value) {
       uint32_t n10 = 0;
       encode_pairs_1d<0, 31>(P, n10, wr);
+      return;
+    }
+    if constexpr (DIMS == 3 && kEncodeAhead32) {
+      const uint32_t r0 = (uint32_t)P.template get<0>(31);
+      uint32_t e0 = wr.sp0(byte_off4<0>(r0)), e1 = wr.sp1(byte_off4<1>(r0));
+      encode_planes_ahead<0, 31, true, false>(P, n, e0, e1, wr);
       return;
     }
     encode_half_fixed<0, 31>(P, n, wr);
