@@ -252,7 +252,6 @@ using reg_writer = typename std::conditional<REG == 1 && !traits<Scalar>::is_int
 template <bool PRIO = true>
 struct LdsReader {
   static constexpr bool kPrio = PRIO;
-  static constexpr bool kAhead = true;  // the plane loops read the windows a step ahead (decode_plane_ahead)
   const uint32_t* lds32;
   const uint32_t* lut32;  // the workgroup's copy of the chunk tables (static LDS)
   const uint16_t* d1d;    // 1D: the workgroup's plane table (Plane1dDecLut)
@@ -388,7 +387,6 @@ struct LdsReader {
 // the 4-byte entries (one AND instead of a shift and an AND).
 template <bool PRIO = true, bool B32 = false>
 struct RegReader : LdsReader<PRIO> {
-  static constexpr bool kAhead = false;  // windows are shifts of a register: nothing to read ahead
   uint64_t blk, blk4;
   __device__ __forceinline__ void set_block(uint64_t b) {
     blk = b;

@@ -82,7 +82,6 @@ ZFP_HD uint64_t lowmask(unsigned n) { return n >= 64 ? ~0ull : ((1ull << n) - 1)
 ZFP_HD unsigned ctz64(uint64_t x) { return (unsigned)__builtin_ctzll(x); }  // x != 0
 
 ZFP_HD unsigned umin(unsigned a, unsigned b) { return a < b ? a : b; }
-ZFP_HD unsigned umax(unsigned a, unsigned b) { return a > b ? a : b; }
 
 // ---------------------------------------------------------------------------
 // Coefficient order (zfp-0.5.0/src/template/codec{1,2,3}.c; the same tables
@@ -904,94 +903,6 @@ ZFP_HD bool encode_half_fixed(const planes<UInt, DIMS>& P, unsigned& n, Writer& 
   return true;
 }
 
-#ifdef CUZFP_ENC_AHEAD32
-constexpr bool kEncodeAhead32 = true;  // (timing builds: 32-bit coefficients too)
-#else
-constexpr bool kEncodeAhead32 = false;
-#endif
-#ifndef CUZFP_NO_AHEAD
-constexpr bool kEncodeAhead = true;
-#else
-constexpr bool kEncodeAhead = false;  // (timing builds: encode_half_fixed for 64-bit 3D planes too)
-#endif
-
-// bit length of a 64-bit r (0 for 0): 64 - clz(hi) by the saturating
-// subtraction (0 when hi = 0, see bitlen16), else the low word's
-ZFP_HD uint32_t bitlen64(uint64_t r) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  uint32_t e;
-  asm("v_ffbh_u32 %0, %1\n\tv_sub_u32_e64 %0, 64, %0 clamp" : "=&v"(e) : "v"((uint32_t)(r >> 32)));
-  return umax(e, bitlen16((uint32_t)r));
-#else
-  return r ? 64u - (uint32_t)__builtin_clzll(r) : 0u;
-#endif
-}
-
-// 3D planes of 64-bit coefficients (f64 / int64, compile-time plane numbers):
-// the plane loop runs at two waves a SIMD and waits on latency, not issue, so
-// the next plane's spread lookups are issued a step ahead.  The next n is
-// n + bitlen(r) (less the implied one) whichever step codes this plane, so it
-// is known before this plane's code is built; e0 / e1 carry the entries of
-// r's bytes 0 and 1 into the step that uses them (unused by the wide step).
-// Planes (H, C) .. (0, 0); false once the block is full (as encode_half_fixed).
-// EXACT = false (32-bit coefficients, timing builds): the next n from r's
-// low 16 bits (bitlen16, exact where the one-put step runs); after a wide step
-// the next plane's entries are read again with the n it leaves.
-template <int H, int C, bool PRI, bool EXACT = true, typename UInt, typename Writer>
-ZFP_HD bool encode_planes_ahead(const planes<UInt, 3>& P, unsigned& n, uint32_t& e0, uint32_t& e1, Writer& wr) {
-  if constexpr (C < 0) {
-    if constexpr (H > 0) return encode_planes_ahead<H - 1, 31, false, EXACT>(P, n, e0, e1, wr);
-    return true;
-  } else {
-    if constexpr (C & 1) {  // a pair's first plane: the budget test, as encode_half_fixed
-      if (!any_lane(!wr.full())) return false;
-      wr.settle();
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(CUZFP_NO_PRIO)
-      if constexpr (prio_of<Writer>::value && PRI) {
-        if constexpr (C == CUZFP_PRIO_T2) __builtin_amdgcn_s_setprio(2);
-        else if constexpr (C == CUZFP_PRIO_T1) __builtin_amdgcn_s_setprio(1);
-        else if constexpr (C == CUZFP_PRIO_T0) __builtin_amdgcn_s_setprio(0);
-      }
-#endif
-    }
-    const uint64_t x = P.template get<H>(C);
-    const unsigned nf = n;
-    const uint64_t r = x >> nf;
-    const uint32_t rl = (uint32_t)r;
-    const uint32_t bl = EXACT ? bitlen64(r) : bitlen16(rl);
-    const PlaneLen pl = plane_len<3>(nf, bl, (uint32_t)__builtin_popcount(rl) + bl);
-    unsigned nn = pl.nn - pl.imp;  // min(n + bitlen(r), 63): the next plane's n
-    uint32_t f0 = 0, f1 = 0;
-    uint64_t xn = 0;
-    if constexpr (C > 0 || H > 0) {
-      xn = C > 0 ? P.template get<H>(C > 0 ? C - 1 : 0) : P.template get<(H > 0 ? H - 1 : 0)>(31);
-      const uint32_t rn = (uint32_t)(xn >> nn);
-      f0 = wr.sp0(byte_off4<0>(rn));
-      f1 = wr.sp1(byte_off4<1>(rn));
-    }
-    const bool ok = (r >> 15) == 0 && pl.len <= 64u;
-    if (__builtin_expect(!any_lane(!ok), 1)) {
-      // encode_plane_one_put with the entries read a step ago
-      uint32_t G = (e0 >> 5) | (e1 << (e0 & 31u));
-      const uint32_t g = low_bits(G, pl.width);
-      wr.put((uint64_t)x ^ ((r ^ (uint64_t)g) << nf), pl.len);
-    } else {
-      unsigned nw = nf;
-      encode_plane_wide(x, nw, wr);
-      if constexpr (!EXACT && (C > 0 || H > 0)) {
-        nn = nw;
-        const uint32_t rn = (uint32_t)(xn >> nn);
-        f0 = wr.sp0(byte_off4<0>(rn));
-        f1 = wr.sp1(byte_off4<1>(rn));
-      }
-    }
-    n = nn;
-    e0 = f0;
-    e1 = f1;
-    return encode_planes_ahead<H, C - 1, PRI, EXACT>(P, n, e0, e1, wr);
-  }
-}
-
 // ---------------------------------------------------------------------------
 // 1D blocks by table (4 coefficients: a plane is a nibble).
 //
@@ -1126,12 +1037,6 @@ ZFP_HD void encode_planes(const planes<UInt, DIMS>& P, unsigned maxprec, Writer&
       encode_pairs_1d<0, 31>(P, n10, wr);
       return;
     }
-    if constexpr (DIMS == 3 && kEncodeAhead32) {
-      const uint32_t r0 = (uint32_t)P.template get<0>(31);
-      uint32_t e0 = wr.sp0(byte_off4<0>(r0)), e1 = wr.sp1(byte_off4<1>(r0));
-      encode_planes_ahead<0, 31, true, false>(P, n, e0, e1, wr);
-      return;
-    }
     encode_half_fixed<0, 31>(P, n, wr);
   } else {
     const int kmin = PREC > (int)maxprec ? PREC - (int)maxprec : 0;
@@ -1139,13 +1044,6 @@ ZFP_HD void encode_planes(const planes<UInt, DIMS>& P, unsigned maxprec, Writer&
       if constexpr (DIMS == 1 && has_pair1d<Writer>::value) {
         uint32_t n10 = 0;
         if (encode_pairs_1d<1, 31>(P, n10, wr)) encode_pairs_1d<0, 31>(P, n10, wr);
-        return;
-      }
-      if constexpr (DIMS == 3 && kEncodeAhead) {
-        // the high half's first plane's entries, then a step ahead throughout
-        const uint32_t r0 = (uint32_t)P.template get<1>(31);
-        uint32_t e0 = wr.sp0(byte_off4<0>(r0)), e1 = wr.sp1(byte_off4<1>(r0));
-        encode_planes_ahead<1, 31, true>(P, n, e0, e1, wr);
         return;
       }
       // the priority schedule over the high half only
@@ -1748,87 +1646,6 @@ ZFP_HD PW decode_plane_fast_any(unsigned& n, Reader& rd) {
   return x;
 }
 
-// The stream windows at read position p (not necessarily rd.pos)
-template <typename Reader>
-ZFP_HD void windows_at(Reader& rd, uint32_t p, unsigned m, uint64_t& w, uint32_t& g) {
-  const auto p0 = rd.pos;
-  rd.pos = p;
-  rd.windows(m, w, g);
-  rd.pos = p0;
-}
-
-// decode_plane_fast_any with the windows read a step ahead (readers over the
-// LDS image, kAhead): w / g come in holding this plane's windows and go out
-// holding the next plane's.  Those are read where the common path leaves the
-// lane -- known from the chunk entries' sum, before the rare test and the
-// merge -- so their LDS round trip overlaps the rest of the step instead of
-// starting the next one.  A lane the rare branch leaves elsewhere reads again.
-template <int DIMS, typename PW, typename Reader>
-ZFP_HD PW decode_plane_ahead(unsigned& n, Reader& rd, uint64_t& w, uint32_t& g) {
-  static_assert(DIMS >= 2, "1D codes fit chunk 1: decode_plane_fast_any");
-  constexpr unsigned N = 1u << (2 * DIMS);
-  const unsigned nf = n;  // <= N-1
-  uint32_t e2a, e2b, e1;
-  rd.chunks_fast(g, e1, e2a, e2b);
-  const uint32_t e2 = keep_if_bit13(bfi_v((uint32_t)((int32_t)e1 >> 31), e2b, e2a), e1);
-  const uint32_t S = e1 + e2;
-  const uint32_t npos = S >> kPosShift & 31u;
-  const uint32_t used = S & kUsedMask;
-  const uint32_t p1 = umin(rd.pos + nf + used, rd.end);
-  const unsigned n1 = nf + npos;
-  uint64_t w1;
-  uint32_t g1;
-  windows_at(rd, p1, n1, w1, g1);
-  if (__builtin_expect(any_lane(and_or(S, kNotEnded, nf + npos) >= N), 0)) {
-    // as decode_plane_fast_any's rare branch
-    const auto pos0 = rd.pos;
-    unsigned bits = rd.end - rd.pos;
-    bool slow;
-    PW x = lut_finish<DIMS, PW>(bits, n, rd, slow, nf, umin(nf, bits), w, e1, e2);
-    n = umin(n, N - 1);
-    if (any_lane(slow)) {
-      if (slow) {
-        rd.init(pos0);
-        n = nf;
-        bits = rd.end - pos0;
-        x = decode_plane<DIMS, PW>(bits, n, rd);
-        n = umin(n, N - 1);
-      }
-    }
-    uint64_t w2;
-    uint32_t g2;
-    rd.windows(n, w2, g2);
-    const bool moved = rd.pos != p1 || n != n1;
-    w = moved ? w2 : w1;
-    g = moved ? g2 : g1;
-    return x;
-  }
-  const uint32_t ones = ((e1 >> kOnesShift) & kChunkMask) |
-                        (((e2 >> kOnesShift) & kChunkMask) << ((e1 >> kPosShift) & 31u));
-  const PW x = merge_at<PW>(nf, ones, w);
-  n = n1;
-  rd.pos = p1;
-  w = w1;
-  g = g1;
-  return x;
-}
-
-// Readers whose windows come from LDS (kAhead): the plane loops read them a
-// step ahead (decode_plane_ahead)
-template <typename T, typename = void> struct ahead_of {
-  static constexpr bool value = false;
-};
-template <typename T> struct ahead_of<T, decltype((void)T::kAhead)> {
-  static constexpr bool value = T::kAhead;
-};
-#ifndef CUZFP_NO_DAHEAD
-constexpr bool kDecodeAhead = true;
-#else
-constexpr bool kDecodeAhead = false;  // (timing builds: the windows read at the step's start)
-#endif
-template <typename Reader, int DIMS>
-constexpr bool dec_ahead() { return kDecodeAhead && ahead_of<Reader>::value && DIMS >= 2; }
-
 // Planes 31 .. cmin of 32-bit half H, two per loop trip, while any lane of the
 // wave has budget (a lane without deposits zeros).  Returns the highest plane
 // left unset (-1: none); those below it are unset too.
@@ -1836,21 +1653,13 @@ template <int H, typename UInt, int DIMS, typename Reader>
 ZFP_HD int decode_half(planes<UInt, DIMS>& P, unsigned& n, int cmin, Reader& rd) {
   typedef typename plane_word<DIMS>::type PW;
   int c = 31;
-  uint64_t w = 0;
-  uint32_t g = 0;
-  if constexpr (dec_ahead<Reader, DIMS>()) rd.windows(n, w, g);
   for (; c - 1 >= cmin; c -= 2) {
     if (!any_lane(rd.pos < rd.end)) return c;
     if constexpr (prio_of<Reader>::value)
       progress_priority<CUZFP_DPRIO_T2, CUZFP_DPRIO_T1, CUZFP_DPRIO_T0>(uniform(c));
     PW xa, xb;
-    if constexpr (dec_ahead<Reader, DIMS>()) {
-      xa = decode_plane_ahead<DIMS, PW>(n, rd, w, g);
-      xb = decode_plane_ahead<DIMS, PW>(n, rd, w, g);
-    } else {
-      xa = decode_plane_fast_any<DIMS, PW>(n, rd);
-      xb = decode_plane_fast_any<DIMS, PW>(n, rd);
-    }
+    xa = decode_plane_fast_any<DIMS, PW>(n, rd);
+    xb = decode_plane_fast_any<DIMS, PW>(n, rd);
     ZFP_STAMP(4);  // diagnostic builds: the last fast pair's end
     const int u = uniform(c);
     P.template set<H>(u, xa);
@@ -1915,33 +1724,6 @@ ZFP_HD int decode_half_fixed(planes<UInt, DIMS>& P, unsigned& n, Reader& rd) {
   return C;
 }
 
-// decode_half_fixed with the windows read a step ahead (decode_plane_ahead);
-// w / g hold the next plane's windows
-template <int H, int C, bool PRI = true, typename UInt, int DIMS, typename Reader>
-ZFP_HD int decode_half_fixed_ahead(planes<UInt, DIMS>& P, unsigned& n, Reader& rd, uint64_t& w, uint32_t& g) {
-  typedef typename plane_word<DIMS>::type PW;
-  if constexpr (C >= 1) {
-    if (!any_lane(rd.pos < rd.end)) {
-      if constexpr (kLazyZero && DIMS == 3) zero_fixed<H, C>(P);
-      return C;
-    }
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(CUZFP_NO_PRIO)
-    if constexpr (prio_of<Reader>::value && PRI) {
-      if constexpr (C == CUZFP_DPRIO_T2) __builtin_amdgcn_s_setprio(2);
-      else if constexpr (C == CUZFP_DPRIO_T1) __builtin_amdgcn_s_setprio(1);
-      else if constexpr (C == CUZFP_DPRIO_T0) __builtin_amdgcn_s_setprio(0);
-    }
-#endif
-    const PW xa = decode_plane_ahead<DIMS, PW>(n, rd, w, g);
-    const PW xb = decode_plane_ahead<DIMS, PW>(n, rd, w, g);
-    ZFP_STAMP(4);
-    P.template set<H>(C, xa);
-    P.template set<H>(C - 1, xb);
-    return decode_half_fixed_ahead<H, C - 2, PRI>(P, n, rd, w, g);
-  }
-  return C;
-}
-
 
 template <int H, typename UInt, int DIMS>
 ZFP_HD void zero_planes(planes<UInt, DIMS>& P, int c) {
@@ -1992,14 +1774,7 @@ ZFP_HD void decode_planes(planes<UInt, DIMS>& P, unsigned budget, unsigned maxpr
       decode_planes_1d<0, 31>(P, n12, rd);
       return;
     }
-    if constexpr (dec_ahead<Reader, DIMS>()) {
-      uint64_t w;
-      uint32_t g;
-      rd.windows(n, w, g);
-      decode_half_fixed_ahead<0, 31>(P, n, rd, w, g);
-    } else {
-      decode_half_fixed<0, 31>(P, n, rd);
-    }
+    decode_half_fixed<0, 31>(P, n, rd);
   } else {
     const int kmin = PREC > (int)maxprec ? PREC - (int)maxprec : 0;
     if constexpr (DIMS == 1 && has_dec1d<Reader>::value) {
@@ -2329,7 +2104,8 @@ ZFP_HD bool decode_block(Scalar* f, unsigned maxbits, Reader& rd) {
     if constexpr (sizeof(Scalar) == 8) {
       // (double)q as fma(hi, 2^32, lo): hi * 2^32 and lo are exact, so the
       // one rounding of the fused sum is the conversion's (the compiler's form
-      // is two conversions, an ldexp and an add)
+      // is two conversions, an ldexp and an add): 256^3 rate 16 decode 54.5 ->
+      // 54.2 us (tools/variants.py, r04_ahead.txt)
 #pragma unroll
       for (int i = 0; i < N; i++) {
         const int64_t v = (int64_t)(Int)q[i];

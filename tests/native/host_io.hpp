@@ -70,9 +70,7 @@ struct HostReader {
   }
   void skip(unsigned n) { pos += n; }
   void init(size_t p) { pos = p; }
-  // table decoder interface (see LdsReader in kernels.hpp); the plane loops
-  // read the windows a step ahead, as over the kernels' LDS image
-  static constexpr bool kAhead = true;
+  // table decoder interface (see LdsReader in kernels.hpp)
   void windows(unsigned m, uint64_t& w, uint32_t& g) {
     w = peek();
     pos += m;
