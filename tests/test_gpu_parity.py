@@ -218,6 +218,7 @@ def test_extreme_blocks(cuda, restatement, dtype):
         a = (rng.standard_normal((12, 8, 8)) * sc).astype(dtype)
         a.flat[::5] = 0
         a[0, 0, 0] = np.inf if sc > 1 else a[0, 0, 0]
+        a[6, 4, 4] = np.nan if sc > 1 else a[6, 4, 4]  # a NaN in another block
         for mb in (restatement.rate_to_maxbits(1, dtype, 3), 512, 1000, 4171):
             words, y = _gpu_roundtrip(a, mb, cuda)
             ref = restatement.compress(a, mb)
