@@ -78,6 +78,20 @@ constexpr size_t kSpreadTabBytes = sizeof(SpreadTab);
 typedef __attribute__((address_space(3))) const uint32_t lds_spread;
 typedef lds_spread* P1dPtr;
 
+// n / d and n % d for a wave-uniform d: shifts when d is a power of two (the
+// words or dwords a block takes at rates 4, 8, 16, ...), the compiler's
+// reciprocal-based division (~15 VALU and a readfirstlane) otherwise
+__device__ __forceinline__ void udivmod_uniform(uint32_t n, uint32_t d, uint32_t& q, uint32_t& r) {
+  if (__builtin_expect((d & (d - 1)) == 0, 1)) {
+    const uint32_t sh = (uint32_t)__builtin_ctz(d);
+    q = n >> sh;
+    r = n & (d - 1);
+  } else {
+    q = n / d;
+    r = n % d;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // LDS bit writers / reader (one lane, one block)
 
@@ -860,8 +874,9 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS, true>::value
       // here gave encode 26.5 us and a faster decode of the still-cached
       // stream at 256^3, step 48.8 us, but a cached stream is the bench's
       // artefact, not a decompressor's).
-      uint32_t s = (2 * lane) / W, j = (2 * lane) % W;
-      const uint32_t ds = 128 / W, dj = 128 % W;
+      uint32_t s, j, ds, dj;
+      udivmod_uniform(2 * lane, W, s, j);
+      udivmod_uniform(128u, W, ds, dj);
       for (uint32_t k = 2 * lane; k < kLanes * W; k += 128) {
         uint4 v;
         const uint64_t a0 = lds[j * 64 + s], a1 = lds[(j + 1) * 64 + s];
@@ -997,8 +1012,9 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) voi
     if (cont) {
       // piece 64 q + lane: dwords j .. j + 3 of block s, 4 (64 q + lane) = s D + j
       uint32_t* L0 = (uint32_t*)lds;
-      uint32_t sb = (4 * lane) / D, j = (4 * lane) % D;
-      const uint32_t dsb = 256 / D, dj = 256 % D;
+      uint32_t sb, j, dsb, dj;
+      udivmod_uniform(4 * lane, D, sb, j);
+      udivmod_uniform(256u, D, dsb, dj);
 #pragma unroll
       for (uint32_t q = 0; q < kHeld; q++)
         if (4 * q < D) {
