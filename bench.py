@@ -93,7 +93,16 @@ def parse():
                    help="test mode, no GPU: every rank runs the gloo backend and the CPU oracle stands in for "
                         "the codec, so the launcher and the rank bookkeeping can be checked on a CPU-only host; "
                         "the line it prints is not a measurement")
-    return p.parse_args()
+    p.add_argument("--dist-init", action="store_true",
+                   help="N = 1: initialise the process group anyway (RCCL with --backend nccl, world size 1) and "
+                        "run the stream all-gathers through it, so RCCL's library load, device binding and "
+                        "all_gather_into_tensor run on a one-GPU box; the gathered stream is checked against "
+                        "the local one")
+    a = p.parse_args()
+    if a.same_device and a.backend != "gloo":
+        # two RCCL ranks on one device are refused or hang inside RCCL: say so at once
+        p.error("--same-device needs --backend gloo (RCCL does not run two ranks on one GPU)")
+    return a
 
 
 def launch_ranks(args) -> int:
@@ -269,6 +278,15 @@ def cpu_baseline(a: np.ndarray, maxbits: int):
                         "decode_GBps": round(s1.nbytes / decc0 / 1e9, 4),
                         "roundtrip_ms": round(rtc0 * 1e3, 3), "maxbits": mb1,
                         "sample": f"median of {reps} single-core round trips"},
+            # the whole host (north star: "the box's own host cores"), not run: the GPU
+            # box caps a job's CPU pools at its GPU's share (OMP_NUM_THREADS), so the
+            # whole-host figure is this share's measured rate scaled by CPUs / threads
+            # (z-slabs are independent; the share's own parallel efficiency is given)
+            "whole_host": {"cpus": aff, "measured": False,
+                           "projected_GBps": round(nbytes / rt / 1e9 * aff / cores, 3),
+                           "share_parallel_efficiency": round((nbytes / rt) / (cores * quarter.nbytes / rt1), 3),
+                           "note": f"linear projection of the {cores}-thread measurement to all {aff} CPUs of the "
+                                   "host; not timed (the box's rules keep a job's CPU pool to its GPU's share)"},
             "wall_s": round(wall, 2)}
 
 
@@ -279,7 +297,7 @@ def allgather_words(zd, words):
     return zd.allgather_stream(words)
 
 
-def run_config5(E: int, steps: int, world: int, rank: int, dev, graphed, dist):
+def run_config5(E: int, steps: int, world: int, rank: int, dev, graphed, dist, use_dist: bool = False):
     """BASELINE configs[4] at this N, GPU phase: one E^3 f32 polynomial
     array at rate 8 strong-scaled over the N ranks as z-slabs of E/N planes.  Each
     rank encodes and decodes its slab (no communication); the step time is the
@@ -353,7 +371,7 @@ def run_config5(E: int, steps: int, world: int, rank: int, dev, graphed, dist):
     torch.cuda.synchronize()
 
     ag_s, full = None, None
-    if world > 1:
+    if use_dist:  # (world 1 with --dist-init: RCCL's one-rank all-gather, a copy)
         full = allgather_words(zd, words)
         torch.cuda.synchronize()
         dist.barrier()
@@ -366,6 +384,8 @@ def run_config5(E: int, steps: int, world: int, rank: int, dev, graphed, dist):
         torch.cuda.synchronize()
         dist.barrier()
         ag_s = allmax(e0.elapsed_time(e1) / 5 * 1e-3)
+        if world == 1:
+            full = None  # the local stream is the gathered one (checked in main's all-gather)
         if rank != 0:
             full = None
     out = zd.sharded_summary(sh, 4, step_s, enc_s, dec_s, HBM_PEAK_GBS, ag_s,
@@ -432,8 +452,14 @@ def main():
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
     backend = "nccl (RCCL)" if args.backend == "nccl" else "gloo (host-copy collectives)"
-    if world > 1:
+    use_dist = world > 1 or args.dist_init
+    if use_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1 and "MASTER_PORT" not in os.environ:
+            import socket
+            with socket.socket() as s_:
+                s_.bind(("127.0.0.1", 0))
+                os.environ["MASTER_PORT"] = str(s_.getsockname()[1])
         if args.backend == "nccl":
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
         else:
@@ -517,7 +543,7 @@ def main():
     c5 = None
     if not args.no_config5 and dims == 3 and args.dtype == "float32" and not strong:
         try:
-            c5 = run_config5(args.config5_edge, args.config5_steps, world, rank, dev, graphed, dist)
+            c5 = run_config5(args.config5_edge, args.config5_steps, world, rank, dev, graphed, dist, use_dist)
         except torch.cuda.OutOfMemoryError as e:  # pragma: no cover
             c5 = {"error": f"out of memory: {e}"}
 
@@ -575,7 +601,7 @@ def main():
 
     # optional RCCL all-gather of the compressed stream (the exchange step)
     allgather = None
-    if world > 1 and zd.uniform_shard_ok(gshape, world, maxbits):
+    if use_dist and zd.uniform_shard_ok(gshape, world, maxbits):
         full = allgather_words(zd, words)
         torch.cuda.synchronize()
         dist.barrier()
@@ -590,8 +616,11 @@ def main():
         ag_s = float(t.item())
         allgather = {"bytes_per_rank_in": int(full.numel() * 8 - nbytes_stream), "ms": round(ag_s * 1e3, 3),
                      "GBps_per_rank_in": round((full.numel() * 8 - nbytes_stream) / ag_s / 1e9, 2),
-                     "backend": backend}
-        del full
+                     "backend": backend, "world_size": world}
+        # this rank's segment of the gathered stream is its own stream, word for word
+        seg = full[rank * words.numel():(rank + 1) * words.numel()]
+        allgather["own_segment_matches"] = bool(torch.equal(seg, words))
+        del full, seg
 
     # (last before the warmup steps: the ~100 ms of back-to-back kernels bring
     # the GPU to the clocks it holds under load, see "Order of the GPU work")
@@ -666,17 +695,24 @@ def main():
     dom_bytes = enc_bytes if dominant == "encode" else dec_bytes
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     workload = f"{dims}d_{args.dtype}_{n}^{dims}_rate{args.rate:g}" + (f"_zslab{world}" if strong and world > 1 else "")
-    traffic = None
+    # roofline.traffic: HBM bytes a launch from rocprofv3 PMC counters, which a
+    # run cannot collect on itself (a --pmc pass is its own profiled run): read
+    # from the builder's PMC session record for this workload, and say which
+    traffic, traffic_source = None, None
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
             wk = workload
             if tj.get("workload") == wk:
                 traffic = tj.get(dominant + "_hbm_bytes_per_launch")
+                traffic_source = {"file": os.path.relpath(args.traffic_json, ROOT), "session": tj.get("source"),
+                                  "method": tj.get("method"),
+                                  "note": "PMC counters of an earlier profiled session of this workload, "
+                                          "not of this run"}
         except Exception:
             traffic = None
 
-    ranks = rank_info(dist, world, dev, backend if world > 1 else "none")
+    ranks = rank_info(dist, world, dev, backend if use_dist else "none")
     result = None
     if rank == 0:
         host_path = None
@@ -753,7 +789,8 @@ def main():
             "decode_GBps_input": round(n_in / (dec_ms * 1e-3) / 1e9, 1),
             "roofline": {"bound": "hbm", "kernel": f"zfp_{dominant}", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "algorithmic_bytes_per_launch": dom_bytes,
+                         "traffic": traffic, "traffic_source": traffic_source,
+                         "algorithmic_bytes_per_launch": dom_bytes,
                          "frac_of_copy": round(achieved / hbm_copy["GBps_1GiB"], 4) if hbm_copy else None},
             "hbm_copy": hbm_copy,
             "cpu_baseline": cpu,
@@ -766,7 +803,7 @@ def main():
             **ranks,
         }
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if use_dist:
         dist.barrier()
         dist.destroy_process_group()
     return result

@@ -107,21 +107,22 @@ constexpr uint32_t kSlackWords = 6;
 template <bool PRIO = true>
 struct LdsOrWriter {
   static constexpr bool kPrio = PRIO;  // progress_priority schedule (zfp_block.hpp)
+  static constexpr bool kZeroInline = true;  // zero blocks coded inline (encode_block)
   uint64_t* p;          // the lane's column: word j at p[64 j], W + kSlackWords words, zeroed
   lds_spread* lut;      // the workgroup's spread tables
   uint32_t pos, lim;    // bits produced; 64 * W
   P1dPtr p1d;           // 1D: the workgroup's pair table (Pair1dLut)
+  uint64_t fit_lim;     // 2^15 - 1 in SGPRs (encode_plane_step's fit test)
   __device__ __forceinline__ uint32_t pair1d(uint32_t o) const { return *(P1dPtr)((uintptr_t)p1d + o); }
   __device__ __forceinline__ bool full() const { return pos >= lim; }
   __device__ __forceinline__ void put(uint64_t v, unsigned n) {  // v < 2^n
     const uint32_t w = pos >> 6;
     uint64_t* q = p + w * 64;
-    // the shifts use the low 6 bits of their counts: pos & 63 and
-    // 63 - (pos & 63) = (pos ^ 63) & 63 (one full-rate XOR)
-    uint64_t lo, hi;
-    asm("v_lshlrev_b64 %0, %1, %2" : "=v"(lo) : "v"(pos), "v"(v));
-    asm("v_lshrrev_b64 %0, 1, %1" : "=v"(hi) : "v"(v));
-    asm("v_lshrrev_b64 %0, %1, %0" : "+v"(hi) : "v"(pos ^ 63u));
+    // the 64-bit shifts use the low 6 bits of their counts: pos & 63 and
+    // 63 - (pos & 63) = (pos ^ 63) & 63 (one full-rate XOR); plain shifts
+    // (an inline-asm shift read by the next one costs an s_nop)
+    const uint64_t lo = v << (pos & 63u);
+    const uint64_t hi = (v >> 1) >> ((pos ^ 63u) & 63u);
     atomicOr((unsigned long long*)&q[0], (unsigned long long)lo);
     atomicOr((unsigned long long*)&q[64], (unsigned long long)hi);
     pos += n;
@@ -131,10 +132,14 @@ struct LdsOrWriter {
   __device__ __forceinline__ uint32_t sp1(uint32_t o) const { return *(lds_spread*)((uintptr_t)(lut + 256) + o); }
   __device__ __forceinline__ uint32_t spread(uint32_t b) const { return lut[256 + b] >> 1; }
   __device__ __forceinline__ void zero_bit() { pos++; }
+  // every LDS access issued so far has completed (s_waitcnt lgkmcnt(0))
+  __device__ __forceinline__ void lds_wait() const { __builtin_amdgcn_s_waitcnt(0xc07f); }
   __device__ __forceinline__ void finish() {}
   // a full lane keeps stepping with its wave: restart it at the first slack
   // row each plane, so its (discarded) pieces stay within rows W .. W + 3
   __device__ __forceinline__ void settle() { pos = pos < lim ? pos : lim; }
+  // a zero block: full from the start, so every bit of it lands in the slack
+  __device__ __forceinline__ void mark_full(bool z) { pos = z ? lim : pos; }
 };
 
 // general maxbits: the lane's bits are [pos0, end) of the wave's segment;
@@ -148,6 +153,7 @@ struct LdsBitWriter {
   uint32_t pos, end, cnt;  // pos: stream offset of acc's bit 0
   uint64_t acc;
   P1dPtr p1d;              // 1D: the workgroup's pair table (Pair1dLut)
+  uint64_t fit_lim;        // 2^15 - 1 in SGPRs (encode_plane_step's fit test)
   __device__ __forceinline__ uint32_t pair1d(uint32_t o) const { return *(P1dPtr)((uintptr_t)p1d + o); }
   __device__ __forceinline__ uint32_t sp0(uint32_t o) const { return *(lds_spread*)((uintptr_t)lut + o); }
   __device__ __forceinline__ uint32_t sp1(uint32_t o) const { return *(lds_spread*)((uintptr_t)(lut + 256) + o); }
@@ -184,6 +190,8 @@ struct LdsBitWriter {
     if (cnt && pos < end) emit(acc);
   }
   __device__ __forceinline__ void settle() {}  // emit() drops bits past maxbits
+  // every LDS access issued so far has completed (s_waitcnt lgkmcnt(0))
+  __device__ __forceinline__ void lds_wait() const { __builtin_amdgcn_s_waitcnt(0xc07f); }
 };
 
 // maxbits <= 64 (1D rate <= 16, 2D rate <= 4: BASELINE's 2D 8192^2 rate 2 and
@@ -213,6 +221,8 @@ struct RegWriter {
   __device__ __forceinline__ void finish() {}
   __device__ __forceinline__ void settle() {}
   __device__ __forceinline__ uint64_t bits() const { return acc & lowmask(mb); }
+  // every LDS access issued so far has completed (s_waitcnt lgkmcnt(0))
+  __device__ __forceinline__ void lds_wait() const { __builtin_amdgcn_s_waitcnt(0xc07f); }
 };
 
 // maxbits 32 for floating-point blocks: a coded block's first stream bit is
@@ -247,6 +257,8 @@ struct RegWriter32 {
   __device__ __forceinline__ void finish() {}
   __device__ __forceinline__ void settle() {}
   __device__ __forceinline__ uint64_t bits() const { return cnt ? (acc << 1) | 1u : 0u; }
+  // every LDS access issued so far has completed (s_waitcnt lgkmcnt(0))
+  __device__ __forceinline__ void lds_wait() const { __builtin_amdgcn_s_waitcnt(0xc07f); }
 };
 
 // the register writer of a maxbits-32 (REG 1) / 64 (REG 2) block
@@ -271,6 +283,7 @@ struct LdsReader {
   const uint16_t* d1d;    // 1D: the workgroup's plane table (Plane1dDecLut)
   uint32_t pos;
   uint32_t end;  // the block's budget end (decode_planes sets it; pos never passes it)
+  uint32_t rare_lim;  // kNotEnded - 1, held in an SGPR (decode_planes sets it)
   uint32_t x0, x1, x2, x3, x4;
   // byte address of the row holding bit p: lds32 + 256 * (p >> 5), in two
   // instructions (the compiler's form of the same expression takes three)
@@ -293,6 +306,28 @@ struct LdsReader {
         ((uint64_t)__builtin_amdgcn_alignbit(a2, a1, pos) << 32);
     g = __builtin_amdgcn_alignbit(b1, b0, q);
   }
+  // The fast plane step's windows, split so that the step waits on the LDS
+  // twice a plane rather than once per value (the compiler's own waits come
+  // before each first use): the group window m bits on, read and waited for
+  // alone (the step's critical path: its chunk lookups need it), then -- after
+  // the chunk lookups are issued -- the 64-bit window at the position, whose
+  // reads land in the lookups' shadow and are waited for with them.
+  __device__ __forceinline__ uint32_t window_g(uint32_t m) const {
+    const uint32_t q = pos + m;
+    lds_u32* t = row(q);
+    const uint32_t b0 = t[0], b1 = t[64];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): vmcnt / expcnt not waited for
+    return __builtin_amdgcn_alignbit(b1, b0, q);
+  }
+  __device__ __forceinline__ WRaw window_w_issue() const {
+    lds_u32* r = row(pos);
+    return WRaw{r[0], r[64], r[128]};
+  }
+  __device__ __forceinline__ uint64_t window_w_make(const WRaw& a) const {
+    return (uint64_t)__builtin_amdgcn_alignbit(a.a1, a.a0, pos) | ((uint64_t)__builtin_amdgcn_alignbit(a.a2, a.a1, pos) << 32);
+  }
+  // every LDS read issued so far has landed (s_waitcnt lgkmcnt(0))
+  __device__ __forceinline__ void lds_wait() const { __builtin_amdgcn_s_waitcnt(0xc07f); }
   // The chunk tables are the kernel's static LDS (address 0), so an entry's
   // byte offset goes straight into ds_read's address with the state in the
   // offset field.  (The plane loops are bound by the count of VALU
@@ -417,6 +452,12 @@ struct RegReader : LdsReader<PRIO> {
     else
       g = (uint32_t)at(this->pos + m);
   }
+  __device__ __forceinline__ uint32_t window_g(uint32_t m) const {
+    if constexpr (B32) return (uint32_t)(blk4 >> (this->pos + m));  // the group window << 2
+    return (uint32_t)at(this->pos + m);
+  }
+  __device__ __forceinline__ WRaw window_w_issue() const { return WRaw{0u, 0u, 0u}; }
+  __device__ __forceinline__ uint64_t window_w_make(const WRaw&) const { return at(this->pos); }
   // (B32: g from windows() is the group window << 2; its bit 2 is the leading
   // test)
   __device__ __forceinline__ void chunks_fast(uint32_t g, uint32_t& e1, uint32_t& e2a, uint32_t& e2b) const {
@@ -442,8 +483,10 @@ struct RegReader : LdsReader<PRIO> {
   }
   __device__ __forceinline__ uint64_t peek() const { return at(this->pos); }
   __device__ __forceinline__ uint32_t window32(uint32_t q) const { return (uint32_t)at(q); }
-  // (B32: pos <= 32, and at pos = 32 the budget is spent, so the lookup is
-  // the c = 0 entry whatever the bits; v_bfe_u32 reads bits past 31 as zeros)
+  // (B32: pos <= 32.  v_bfe_u32 takes its offset mod 32, so at pos = 32 it
+  // reads bits 0-7 of the block, not zeros; that is harmless because pos = 32
+  // means the budget is spent, c = 0, and every c = 0 entry of Plane1dDecLut
+  // is the same whatever the stream bits s)
   __device__ __forceinline__ uint32_t bits8() const {
     if constexpr (B32) return __builtin_amdgcn_ubfe((uint32_t)blk, this->pos, 8u);
     return (uint32_t)(blk >> (this->pos & 63)) & 0xffu;
@@ -689,6 +732,15 @@ constexpr uint32_t kRegBatchMinWaves = CUZFP_REG_BATCH_MIN_WAVES;
 #define CUZFP_REG_BATCH_PRIO 0
 #endif
 
+// The wave's index in its workgroup, as a wave-uniform (SGPR) value: the
+// compiler takes threadIdx.x >> 6 for a per-lane value, so every branch on
+// the wave's number (a wave past the launch's end, a partial last wave) would
+// otherwise be a divergent one, and everything after it an exec-masked region
+// -- an s_cbranch_execz and exec-mask bookkeeping at every step of the coders.
+__device__ __forceinline__ uint32_t wave_in_group() {
+  return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+}
+
 __device__ __forceinline__ void wave_lds_sync() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
@@ -739,7 +791,11 @@ __device__ __forceinline__ void scatter_f64_staged(double* __restrict__ data, co
       st16<true>(row + 2 * lane, stage[j * 128 + lane]);
       st16<true>(row + 128 + 2 * lane, stage[j * 128 + 64 + lane]);
     }
-    // (the next pass's LDS writes follow these reads in the wave's LDS order)
+    // The next pass overwrites the pieces other lanes have just read: its
+    // writes must not be moved above these reads (the compiler sees disjoint
+    // per-lane addresses), so the wave waits for them (asm memory clobber;
+    // at most 16 waits a block)
+    if (r0 + ROWS < 16) wave_lds_sync();
   }
 }
 
@@ -768,7 +824,7 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS, true>::value
   // 1D: the pair table (Pair1dLut, 4 KiB), one copy a workgroup: 16 bytes a lane
   __shared__ __attribute__((aligned(16))) uint32_t ptab[DIMS == 1 ? 1024 : 4];
   constexpr int N = 1 << (2 * DIMS);
-  const uint32_t wig = threadIdx.x >> 6;  // wave in workgroup
+  const uint32_t wig = wave_in_group();
   const uint32_t wave = g.wave0 + blockIdx.x * (blockDim.x >> 6) + wig;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t b = wave * kLanes + lane;
@@ -819,7 +875,13 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS, true>::value
   // slower, round 4: 256^3 r16 encode 51.1 -> 54.5 us with non-temporal
   // loads, 50.9 -> 54.4 us with plain ones; non-temporal hints on these
   // strided row loads: 50.9 -> 55.6 us)
-  if (b < g.nblocks) gather<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
+  if (b < g.nblocks) {
+    gather<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
+  } else if constexpr (ALIGNED && !REG) {
+    // a lane past the last block codes a zero block (see below)
+#pragma unroll
+    for (int i = 0; i < N; i++) f[i] = (Scalar)0;
+  }
   // (one copy a workgroup behind a barrier measured slower: 28.0 -> 28.4 us at 256^3)
   if constexpr (!kGroupSpread) {
 #pragma unroll
@@ -844,16 +906,20 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS, true>::value
     }
     return;
   }
-  if (b < g.nblocks) {
-    if constexpr (ALIGNED) {
-      uint64_t* mine = lds + lane;
-      for (uint32_t j = 0; j < W + kSlackWords; j++) mine[j * 64] = 0;  // own column
-      wave_lds_sync();  // the tables
-      LdsOrWriter<PRIO> wr{mine, lut, 0, 64 * W, p1d};
-      encode_block<Scalar, DIMS>(f, g.maxbits, wr);
-    } else {
+  // ALIGNED: every lane of the wave codes (a lane past the last block holds a
+  // zero block, which LdsOrWriter codes inline into its discarded slack), so
+  // the coder runs outside any per-lane branch; the copy-out moves the live
+  // blocks' words only
+  if constexpr (ALIGNED) {
+    uint64_t* mine = lds + lane;
+    for (uint32_t j = 0; j < W + kSlackWords; j++) mine[j * 64] = 0;  // own column
+    wave_lds_sync();  // the tables
+    LdsOrWriter<PRIO> wr{mine, lut, 0, 64 * W, p1d, uniform_const64(0x7fffu)};
+    encode_block<Scalar, DIMS>(f, g.maxbits, wr);
+  } else if (b < g.nblocks) {
+    {
       wave_lds_sync();  // the tables and the zeroed image
-      LdsBitWriter<PRIO> wr{lds, lut, lane * g.maxbits, (lane + 1) * g.maxbits, 0, 0, p1d};
+      LdsBitWriter<PRIO> wr{lds, lut, lane * g.maxbits, (lane + 1) * g.maxbits, 0, 0, p1d, uniform_const64(0x7fffu)};
       encode_block<Scalar, DIMS>(f, g.maxbits, wr);
     }
   }
@@ -931,7 +997,7 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) voi
                                                                       Scalar* __restrict__ data) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds_all[];
   constexpr int N = 1 << (2 * DIMS);
-  const uint32_t wig = threadIdx.x >> 6;
+  const uint32_t wig = wave_in_group();
   const uint32_t wave = g.wave0 + blockIdx.x * (blockDim.x >> 6) + wig;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t b = wave * kLanes + lane;
@@ -1059,6 +1125,9 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) voi
         // the block reads as zeros past its last bit (the plane steps rely on it)
         if (g.maxbits & 31) L[(D - 1) * 64] &= (1u << (g.maxbits & 31)) - 1u;
       }
+    } else if (wave < g.wave_end) {
+      // a lane past the last block decodes a zero block (its stores are skipped)
+      for (uint32_t j = 0; j < D; j++) L[j * 64] = 0;
     }
     if (wave < g.wave_end)
       for (uint32_t j = D; j < D + 5; j++) L[j * 64] = 0;
@@ -1071,9 +1140,12 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) voi
   ZFP_STAMP(0);
   wave_lds_sync();
   ZFP_STAMP(5);
-  if (b < g.nblocks) {
+  // Every lane of a live wave decodes (a lane past the last block reads a
+  // zero block), so the coder runs outside any per-lane branch; only the
+  // stores are guarded.
+  {
     Scalar f[N];
-    bool coded;
+    bool coded;  // false only for a wave of zero blocks (decode_block)
     if constexpr (REG) {
       RegReader<PRIO, REG == 32> rd;
       rd.lds32 = L;
@@ -1106,13 +1178,15 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) voi
         return;
       }
     }
-    if (coded) {
-      scatter<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
-    } else {  // a zero block
-      Scalar z[N];
+    if (b < g.nblocks) {
+      if (coded) {
+        scatter<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
+      } else {  // a wave of zero blocks
+        Scalar z[N];
 #pragma unroll
-      for (int i = 0; i < N; i++) z[i] = (Scalar)0;
-      scatter<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), z);
+        for (int i = 0; i < N; i++) z[i] = (Scalar)0;
+        scatter<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), z);
+      }
     }
   }
   ZFP_STAMP(6);
@@ -1130,7 +1204,7 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS, true>::value
   constexpr int N = 1 << (2 * DIMS);
   __shared__ __attribute__((aligned(16))) uint32_t stab[512];  // LDS address 0 (static)
   __shared__ __attribute__((aligned(16))) uint32_t ptab[DIMS == 1 ? 1024 : 4];
-  const uint32_t wig = threadIdx.x >> 6;
+  const uint32_t wig = wave_in_group();
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t w0 = g.wave0 + (blockIdx.x * WPG + wig) * K;
   Scalar f[K][N];
@@ -1204,7 +1278,7 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) voi
   constexpr int N = 1 << (2 * DIMS);
   __shared__ __attribute__((aligned(16))) uint32_t ctab[kChunkLutBytes / 4];  // LDS address 0 (static)
   __shared__ __attribute__((aligned(16))) uint16_t dtab[DIMS == 1 ? sizeof(Plane1dDecLut) / 2 : 8];
-  const uint32_t wig = threadIdx.x >> 6;
+  const uint32_t wig = wave_in_group();
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t w0 = g.wave0 + (blockIdx.x * WPG + wig) * K;
   uint64_t q[K];
@@ -1229,23 +1303,23 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) voi
 #pragma unroll
     for (int j = 0; j + 1 < K; j++) q[j] = q[j + 1];  // the next batch's words move up (static registers)
     const uint32_t b = (w0 + k) * kLanes + lane;
-    if (b < g.nblocks) {
-      if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);  // lowered through the plane loop (progress_priority)
-      Scalar f[N];
-      RegReader<PRIO, REG == 32> rd;
-      rd.lds32 = nullptr;
-      rd.lut32 = ctab;
-      rd.d1d = dtab;
-      rd.set_block(blk);
-      rd.init(0);
-      const bool coded = decode_block<Scalar, DIMS>(f, g.maxbits, rd);
-      if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);
-      if (!coded) {
+    // every lane decodes (a lane past the last block holds a zero block: its
+    // word is 0); only the stores are guarded
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);  // lowered through the plane loop (progress_priority)
+    Scalar f[N];
+    RegReader<PRIO, REG == 32> rd;
+    rd.lds32 = nullptr;
+    rd.lut32 = ctab;
+    rd.d1d = dtab;
+    rd.set_block(blk);
+    rd.init(0);
+    const bool coded = decode_block<Scalar, DIMS>(f, g.maxbits, rd);  // false: a wave of zero blocks
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);
+    if (!coded) {
 #pragma unroll
-        for (int i = 0; i < N; i++) f[i] = (Scalar)0;
-      }
-      scatter<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
+      for (int i = 0; i < N; i++) f[i] = (Scalar)0;
     }
+    if (b < g.nblocks) scatter<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
   }
 }
 

@@ -79,6 +79,53 @@ template <> struct nbmask<uint64_t> { static constexpr uint64_t value = 0xaaaaaa
 
 ZFP_HD uint64_t lowmask(unsigned n) { return n >= 64 ? ~0ull : ((1ull << n) - 1); }
 
+// the raw dwords of a reader's 64-bit window (LDS readers: issued, not yet
+// combined; register readers: unused)
+struct WRaw {
+  uint32_t a0, a1, a2;
+};
+
+// The scheduler may not move instructions across this point (device builds):
+// keeps the fast step's LDS reads issued in order and its uses of them after
+// the one wait that covers them all.
+ZFP_HD void sched_fence() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_sched_barrier(0);
+#endif
+}
+
+// x, opaque to the optimizer (an empty asm: no instruction, no hazard
+// padding).  Stops instruction selection from seeing through a mask -- e.g.
+// turning a v_bfi_b32 with a sign-splat mask into a compare and a VCC
+// v_cndmask_b32 (a ~17-cycle issue), or dropping a v_bfi_b32's mask it can
+// prove redundant in favour of two instructions.
+ZFP_HD uint32_t launder(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("" : "+v"(x));
+#endif
+  return x;
+}
+// a wave-uniform constant the compiler keeps in one SGPR instead of
+// re-materialising it (s_movk) wherever it is used
+ZFP_HD uint32_t uniform_const(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("" : "+s"(x));
+#endif
+  return x;
+}
+ZFP_HD uint64_t uniform_const64(uint64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("" : "+s"(x));
+#endif
+  return x;
+}
+ZFP_HD uint64_t launder(uint64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("" : "+v"(x));
+#endif
+  return x;
+}
+
 ZFP_HD unsigned ctz64(uint64_t x) { return (unsigned)__builtin_ctzll(x); }  // x != 0
 
 ZFP_HD unsigned umin(unsigned a, unsigned b) { return a < b ? a : b; }
@@ -325,13 +372,75 @@ ZFP_HD uint32_t perm_bytes(uint32_t b, uint32_t a, uint32_t sel) {
 //              (decoder: the odd planes again, now as bits of coefficients).
 // Either is the "^ 0xaaaa..." of the negabinary conversion, at no cost.
 enum { kInvNone = 0, kOddWords = 1, kOddBits = 2 };
+
+// Two words shifted by one 64-bit instruction (bit-granular stages): the bits
+// one word's shift moves into the other lie where the stage's mask drops them
+// -- ~m has its low J bits clear (the left shifts' spill), m its top J bits
+// (the right shifts') -- so a pair of 32-bit shifts becomes one v_lshlrev_b64 /
+// v_lshrrev_b64 on the two words as a register pair.
+// (The shift count goes in as an SGPR the optimizer cannot see through: a
+// 64-bit shift by a known constant is split by the compiler into 32-bit shifts
+// and a funnel shift, and an inline-asm shift makes the hazard recognizer pad
+// each consumer with an s_nop.)
+template <int J>
+ZFP_HD uint32_t opaque_shift() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t s;
+  asm("s_mov_b32 %0, %1" : "=s"(s) : "i"(J));
+  return s;
+#else
+  return J;
+#endif
+}
+template <int J>
+ZFP_HD void shl2(uint32_t& x, uint32_t& y, uint32_t sj) {
+  const uint64_t r = ((uint64_t)x | ((uint64_t)y << 32)) << sj;
+  x = (uint32_t)r;
+  y = (uint32_t)(r >> 32);
+}
+template <int J>
+ZFP_HD void shr2(uint32_t& x, uint32_t& y, uint32_t sj) {
+  const uint64_t r = ((uint64_t)x | ((uint64_t)y << 32)) >> sj;
+  x = (uint32_t)r;
+  y = (uint32_t)(r >> 32);
+}
+
 template <int J, int INV = kInvNone>
 ZFP_HD void transpose_stage(uint32_t* a, int rows) {
   // swap the J x J off-diagonal sub-blocks of every 2J x 2J tile:
   //   lo' = (lo & m) | ((hi << J) & ~m),  hi' = ((lo >> J) & m) | (hi & ~m)
-  // one v_perm_b32 per word for the byte-granular stages, two ops otherwise
+  // one v_perm_b32 per word for the byte-granular stages; the bit-granular
+  // ones take two pairs (i, i + J), (i2, i2 + J) at a time, their shifts as
+  // one 64-bit shift of the two hi words and one of the two lo words, then a
+  // v_bfi_b32 per output word: 3 instructions a pair instead of 4
   constexpr uint32_t m = J == 16 ? 0x0000ffffu : J == 8 ? 0x00ff00ffu : J == 4 ? 0x0f0f0f0fu
                        : J == 2 ? 0x33333333u : 0x55555555u;
+  if constexpr (J <= 4) {
+    // the partner pair: i + 1 for J >= 2 (adjacent words), i + 2 for J = 1
+    constexpr int D = J == 1 ? 2 : 1;
+    const uint32_t sj = opaque_shift<J>();
+#pragma unroll
+    for (int i = 0; i < 32; i++) {
+      if (i >= rows || (i & J) || (i & D)) continue;
+      const int i2 = i + D;
+      uint32_t h1 = a[i + J], h2 = a[i2 + J], l1 = a[i], l2 = a[i2];
+      const uint32_t H1 = h1, H2 = h2;  // hi words as they were
+      shl2<J>(h1, h2, sj);              // hi << J
+      shr2<J>(l1, l2, sj);              // lo >> J
+      if constexpr (INV == kOddBits) {  // J = 1, m = 0x5555...: the odd bits come from hi
+        a[i] = bfi_notb(m, a[i], h1);
+        a[i2] = bfi_notb(m, a[i2], h2);
+        a[i + J] = bfi_notb(m, l1, H1);
+        a[i2 + J] = bfi_notb(m, l2, H2);
+      } else {
+        a[i] = bfi(m, a[i], h1);
+        a[i2] = bfi(m, a[i2], h2);
+        a[i + J] = INV == kOddWords ? nbfi(m, l1, H1) : bfi(m, l1, H1);
+        a[i2 + J] = INV == kOddWords ? nbfi(m, l2, H2) : bfi(m, l2, H2);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 32; i++) {
     if (i >= rows || (i & J)) continue;
@@ -592,6 +701,17 @@ template <typename T> struct prio_of<T, decltype((void)T::kPrio)> {
 // Writers whose put() keeps only the low 32 bits of its value (kPut32: the
 // register writer of a 32-bit block), and the exponent field's put (head(),
 // where a writer has one)
+// Writers that code a zero block inline (kZeroInline): the block is marked
+// full (mark_full) and the coder runs on zero coefficients with the wave, its
+// writes all landing in the lane's discarded slack -- so the coder is not
+// nested in a per-lane branch (LdsOrWriter)
+template <typename T, typename = void> struct zero_inline_of {
+  static constexpr bool value = false;
+};
+template <typename T> struct zero_inline_of<T, decltype((void)T::kZeroInline)> {
+  static constexpr bool value = T::kZeroInline;
+};
+
 template <typename T, typename = void> struct put32_of {
   static constexpr bool value = false;
 };
@@ -761,9 +881,15 @@ ZFP_HD void encode_plane_one_put(PW x, unsigned nf, uint64_t r, const PlaneLen& 
   const uint32_t width = pl.width;
   // "1" + r with every one doubled: one table entry a byte of r (3D: r < 2^15,
   // 2D: r < 2^16; where r's top bits move past bit 31 they lie past width)
+  // both table reads, then one wait for both (the compiler would wait for
+  // each before its first use: two s_waitcnt a plane)
   const uint32_t e0 = wr.sp0(byte_off4<0>(rl));
+  const uint32_t e1 = N > 4 ? wr.sp1(byte_off4<1>(rl)) : 0u;
+  sched_fence();
+  wr.lds_wait();
+  sched_fence();
   uint32_t G = e0 >> 5;
-  if constexpr (N > 4) G |= wr.sp1(byte_off4<1>(rl)) << (e0 & 31u);
+  if constexpr (N > 4) G |= e1 << (e0 & 31u);
   const uint32_t g = low_bits(G, width);
   if constexpr (N <= 16 && put32_of<Writer>::value) {
     // the writer keeps 32 bits of the code (a 32-bit block: the rest lies past
@@ -848,7 +974,9 @@ ZFP_HD void encode_plane_step(PW x, unsigned& n, Writer& wr) {
     // one put while every lane's code fits 64 bits with r < 2^15 (3D rate 8
     // on smooth data: ~26 of ~29 plane steps, tools/coder_stats.cpp);
     // otherwise the wide step for the whole wave
-    const bool ok = (r >> 15) == 0 && pl.len <= 64u;
+    // (r < 2^15 against the writer's fit_lim = 2^15 - 1, a 64-bit constant
+    // kept in SGPRs rather than re-materialised every step)
+    const bool ok = (uint64_t)r <= wr.fit_lim && pl.len <= 64u;
     if (__builtin_expect(!any_lane(!ok), 1))
       encode_plane_one_put<DIMS>(x, nf, r, pl, n, wr);
     else
@@ -1332,9 +1460,10 @@ ZFP_HD uint64_t lowmask64(unsigned m) { return m ? ~0ull >> ((64u - m) & 63u) : 
 template <typename PW>
 ZFP_HD PW merge_at(uint32_t s, uint64_t ones, uint64_t w) {
   if constexpr (sizeof(PW) == 8) {
-    const uint64_t hi = ~0ull << s, o = ones << s;
-    return (PW)bfi_v((uint32_t)hi, (uint32_t)o, (uint32_t)w) |
-           ((PW)bfi_v((uint32_t)(hi >> 32), (uint32_t)(o >> 32), (uint32_t)(w >> 32)) << 32);
+    // (s <= 63: the shifts' counts need no mask; o laundered, or the
+    // compiler drops the mask o already satisfies and ORs it in separately)
+    const uint64_t hi = ~0ull << (s & 63u), o = launder(ones << (s & 63u));
+    return (o & hi) | (w & ~hi);
   } else {
     // 16-bit planes (2D: s <= 15, ones below bit 16 - s): the low s bits of w
     // (one v_bfe_u32) under the shifted ones (one v_lshl_or_b32)
@@ -1350,6 +1479,15 @@ ZFP_HD uint32_t and_or(uint32_t a, uint32_t m, uint32_t c) {
   return r;
 #else
   return (a & m) | c;
+#endif
+}
+
+// all ones when bit B of e is set, else 0 (one v_bfe_i32)
+ZFP_HD uint32_t sbfe1(uint32_t e, int B) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return (uint32_t)__builtin_amdgcn_sbfe((int)e, (unsigned)B, 1u);
+#else
+  return (e >> B) & 1u ? ~0u : 0u;
 #endif
 }
 
@@ -1580,23 +1718,34 @@ ZFP_HD PW decode_plane_any(unsigned& n, Reader& rd) {
 // reads the same bits as n = N), so the window offset and the verbatim mask
 // take n as it is.  Common case: the code ends within the two chunks, below
 // position N-1 (one wave-uniform test covers both).
+
+
 template <int DIMS, typename PW, typename Reader>
 ZFP_HD PW decode_plane_fast_any(unsigned& n, Reader& rd) {
   constexpr unsigned N = 1u << (2 * DIMS);
   const unsigned nf = n;  // <= N-1
-  uint64_t w;
-  uint32_t g;
-  rd.windows(nf, w, g);
-  uint32_t e1, e2;
-  if constexpr (DIMS == 1) {
+  // the group window first (the lookups wait on it), the verbatim window's
+  // reads after the lookups' (Reader::window_g / window_w)
+  const uint32_t g = rd.window_g(nf);
+  uint32_t e1, e2, e2a = 0, e2b = 0;
+  if constexpr (DIMS == 1)
     e1 = rd.chunk1_fast(g);  // a 1D code fits chunk 1
+  else
+    rd.chunks_fast(g, e1, e2a, e2b);
+  const WRaw wr = rd.window_w_issue();
+  sched_fence();
+  rd.lds_wait();  // one wait for the lookups and the window
+  sched_fence();
+  const uint64_t w = rd.window_w_make(wr);
+  if constexpr (DIMS == 1) {
     e2 = 0;
   } else {
-    uint32_t e2a, e2b;
-    rd.chunks_fast(g, e1, e2a, e2b);
-    // the exit state (bit 31) as a mask by one arithmetic shift, the select
-    // by v_bfi (a compare and a v_cndmask otherwise: two slow-issue VALU ops)
-    e2 = keep_if_bit13(bfi_v((uint32_t)((int32_t)e1 >> 31), e2b, e2a), e1);
+    // the exit state (bit 31) as a mask by one arithmetic shift selects the
+    // chunk-2 entry, and bit 13 of chunk 1 (not ended) keeps it: plain
+    // expressions (an inline-asm result read by the next VALU instruction
+    // costs an s_nop), the mask laundered so that it stays a bit select
+    const uint32_t st = launder((uint32_t)((int32_t)e1 >> 31));
+    e2 = ((e2b & st) | (e2a & ~st)) & sbfe1(e1, 13);
   }
   const uint32_t S = e1 + e2;
   const uint32_t npos = S >> kPosShift & 31u;
@@ -1604,7 +1753,12 @@ ZFP_HD PW decode_plane_fast_any(unsigned& n, Reader& rd) {
   // One wave-uniform test for both rare cases: a code longer than the two
   // chunks (the sum carries the marker) and one reaching position N-1
   // (nf + npos >= N; nf + npos < 2N).
-  if (__builtin_expect(any_lane(and_or(S, kNotEnded, nf + npos) >= N), 0)) {
+  // (As one compare: used | (nf + npos) << (13 - 2 DIMS) reaches 2^13 exactly
+  // when used carries the marker or nf + npos >= N -- both parts are below
+  // 2^14, and below 2^13 otherwise.  One v_lshl_or_b32 with inline constants:
+  // a 0x2000 mask would need an SGPR reloaded every plane.)
+  const uint32_t nfp = nf + npos;
+  if (__builtin_expect(any_lane((used | (nfp << (13 - 2 * DIMS))) > rd.rare_lim), 0)) {
     // The budget-aware resolution from the entries already read
     // (lut_finish) for the whole wave, and for the lanes it cannot finish
     // (none on the bench fields: tools/dec_paths.cpp) the general decoder.
@@ -1627,6 +1781,9 @@ ZFP_HD PW decode_plane_fast_any(unsigned& n, Reader& rd) {
         n = umin(n, N - 1);
       }
     }
+    // leave no LDS read of the rare paths in flight: the common path's wait
+    // bookkeeping after the join then needs no extra waits of its own
+    rd.lds_wait();
     return x;
   }
   ZFP_COUNT_PATH(0);
@@ -1641,7 +1798,7 @@ ZFP_HD PW decode_plane_fast_any(unsigned& n, Reader& rd) {
                         (((e2 >> kOnesShift) & kChunkMask) << ((e1 >> kPosShift) & 31u));
   // bits >= nf of the plane from the group code, below it verbatim
   const PW x = merge_at<PW>(nf, ones, w);
-  n = nf + npos;
+  n = nfp;
   rd.pos = umin(rd.pos + nf + used, rd.end);
   return x;
 }
@@ -1764,6 +1921,7 @@ ZFP_HD void decode_planes(planes<UInt, DIMS>& P, unsigned budget, unsigned maxpr
   constexpr int PREC = (int)sizeof(UInt) * 8;
   unsigned n = 0;
   rd.end = rd.pos + budget;  // the reader never passes it
+  rd.rare_lim = uniform_const(kNotEnded - 1u);  // decode_plane_fast_any's rare test
   if constexpr (!(kLazyZero && DIMS == 3)) P.zero();
   if constexpr (PREC == 32) {
     // every plane down to 0 (see encode_planes); the early exits of the
@@ -1976,7 +2134,18 @@ ZFP_HD void encode_block(const Scalar* f, unsigned maxbits, Writer& wr) {
     ZFP_STAMP(1);
     maxprec = precision<DIMS>(emax, T::prec);
     const unsigned e = maxprec ? (unsigned)(emax + T::ebias) : 0u;
-    if (!e) {  // all-zero block: a single 0 bit, then padding
+    // all-zero block: a single 0 bit, then padding (encode.c:206-215)
+    bool zero = !e;
+    if constexpr (zero_inline_of<Writer>::value) {
+      // ... coded inline: marked full (its bits all go to the discarded
+      // slack, its column stays zero), quantised with a zero scale (q = 0);
+      // a wave of zero blocks returns at once
+      if (!any_lane(!zero)) {
+        wr.finish();
+        return;
+      }
+      wr.mark_full(zero);
+    } else if (zero) {
       wr.finish();
       return;
     }
@@ -1985,10 +2154,11 @@ ZFP_HD void encode_block(const Scalar* f, unsigned maxbits, Writer& wr) {
     // gives INT_MIN.  That happens when 2^sh overflows (max |x| < 2^-97 for
     // f32, 2^-961 for f64) and in blocks holding inf or NaN; see
     // oracle/zfp_oracle.c.
-    const Scalar s = (Scalar)fp<Scalar>::pow2(T::prec - 2 - emax);
+    Scalar s = (Scalar)fp<Scalar>::pow2(T::prec - 2 - emax);
+    if constexpr (zero_inline_of<Writer>::value) s = zero ? (Scalar)0 : s;
 #if defined(__HIP_DEVICE_COMPILE__)
     if constexpr (sizeof(Scalar) == 4 && N % 2 == 0) {
-      quantize_f32<N>((const float*)f, (float)s, finite && emax >= -97, (uint32_t*)q);
+      quantize_f32<N>((const float*)f, (float)s, finite && (emax >= -97 || zero), (uint32_t*)q);
     } else
 #endif
     {
@@ -2029,9 +2199,11 @@ ZFP_HD void encode_block(const Scalar* f, unsigned maxbits, Writer& wr) {
   wr.finish();
 }
 
-// Returns false, leaving f untouched, for a zero block (the caller stores
-// zeros: zeroing f here costs the kernel 64 register moves a wave, made on
-// every path before the branch).
+// Returns false, leaving f untouched, when every lane of the wave holds a
+// zero block (the caller stores zeros: zeroing f here costs the kernel 64
+// register moves a wave, made on every path before the branch); a zero block
+// beside coded ones decodes to +0 values (see below).  On the host a "wave"
+// is one lane.
 template <typename Scalar, int DIMS, typename Reader>
 ZFP_HD bool decode_block(Scalar* f, unsigned maxbits, Reader& rd) {
   typedef traits<Scalar> T;
@@ -2043,11 +2215,18 @@ ZFP_HD bool decode_block(Scalar* f, unsigned maxbits, Reader& rd) {
   if constexpr (!T::is_int) {
     // decode.c:352-381
     const uint64_t head = rd.peek();
-    if (!(head & 1)) return false;
+    const bool coded = head & 1;
+    // A zero block (decode.c:354-355) takes the coded path with no budget
+    // inside a wave that holds coded blocks: it reads no planes, so its q
+    // are zero and its values 0 * 2^(emax-p+2) = +0 whatever its header bits
+    // -- the reference's zero block -- and the plane loop is not nested in a
+    // per-lane branch (whose exec-mask bookkeeping costs every plane step).
+    // A wave of zero blocks returns at once.
+    if (!any_lane(coded)) return false;
     emax = (int)((head >> 1) & lowmask(T::ebits)) - T::ebias;
     rd.skip(T::ebits + 1);
     maxprec = precision<DIMS>(emax, T::prec);
-    budget = maxbits - (T::ebits + 1);
+    budget = coded ? maxbits - (T::ebits + 1) : 0u;
   }
   UInt u[N];
 #if defined(CUZFP_PROBE) && CUZFP_PROBE == 2

@@ -14,6 +14,7 @@
 struct HostWriter {
   uint64_t* s;
   size_t pos, end;
+  uint64_t fit_lim = 0x7fff;  // (see LdsOrWriter)
   bool full() const { return pos >= end; }
   void put(uint64_t v, unsigned n) {
     if (pos >= end) return;
@@ -32,6 +33,7 @@ struct HostWriter {
     if (pos < end) pos++;
   }
   void finish() {}
+  void lds_wait() const {}
   uint32_t spread(uint32_t b) const {
     static const cuzfp::SpreadLut t = cuzfp::make_spread_lut();
     return t.e[b];
@@ -54,6 +56,7 @@ struct HostReader {
   size_t words;
   size_t pos;
   size_t end;  // the block's last bit + 1: the stream reads as zeros from there (as on the GPU)
+  uint32_t rare_lim;  // (see LdsReader)
   uint64_t word(size_t i) const { return i < words ? s[i] : 0; }
   uint64_t peek() const {
     if (pos >= end) return 0;
@@ -77,6 +80,15 @@ struct HostReader {
     g = (uint32_t)peek();
     pos -= m;
   }
+  uint32_t window_g(unsigned m) {
+    pos += m;
+    const uint32_t g = (uint32_t)peek();
+    pos -= m;
+    return g;
+  }
+  cuzfp::WRaw window_w_issue() const { return cuzfp::WRaw{0u, 0u, 0u}; }
+  uint64_t window_w_make(const cuzfp::WRaw&) const { return peek(); }
+  void lds_wait() const {}
   // the 1D plane table (o: byte offset) and the next 8 stream bits
   uint32_t dec1d(uint32_t o) const {
     static const cuzfp::Plane1dDecLut t = cuzfp::make_plane1d_dec_lut();

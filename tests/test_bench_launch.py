@@ -73,3 +73,33 @@ def test_gpus2_gloo_same_device_bench():
     assert c5["parity"]["stream_matches_reference"] is True
     assert c5["allgather"]["backend"].startswith("gloo")
     assert d["allgather"] is not None and d["value"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(290)
+def test_rccl_one_rank_bench():
+    """bench.main() through its RCCL branch on a one-GPU box (--dist-init):
+    init_process_group("nccl", world_size=1, device_id=cuda:0), the headline's
+    and configs[4]'s stream all-gathers on RCCL, the gathered segment equal to
+    the local stream.  Not a scaling measurement (one rank)."""
+    r = _run(["--gpus", "1", "--dist-init", "--steps", "10", "--warmup", "2", "--no-cpu-baseline",
+              "--no-host-path", "--no-copy-probe", "--config5-steps", "2", "--kernel-ms", "5"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and d["world_size_seen"] == 1
+    assert d["backend"].startswith("nccl")
+    ag = d["allgather"]
+    assert ag is not None and ag["backend"].startswith("nccl") and ag["own_segment_matches"] is True
+    c5 = d["config5"]
+    assert c5["allgather"]["backend"].startswith("nccl")
+    assert c5["parity"]["stream_matches_reference"] is True
+    assert d["parity"].startswith("stream and decoded sha256 == reference")
+
+
+def test_same_device_needs_gloo():
+    # two RCCL ranks on one GPU are refused at argument parsing (ADVICE r04)
+    r = _run(["--gpus", "2", "--same-device", "--steps", "1", "--warmup", "0"])
+    assert r.returncode != 0
+    assert "--same-device needs --backend gloo" in r.stderr

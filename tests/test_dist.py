@@ -133,6 +133,58 @@ def test_gpu_slabs_allgather(restatement):
         assert np.array_equal(results[r][1], back[z0:z1])
 
 
+def _rccl_one_rank_worker(port, shape, maxbits, q):
+    # RCCL itself on a one-GPU box: a world-size-1 "nccl" process group bound
+    # to cuda:0 (init_process_group(..., device_id=...) as bench.py does), the
+    # HIP encode, and allgather_stream's all_gather_into_tensor on the device
+    # words -- the calls a multi-GPU run makes, with one rank
+    import torch
+    import torch.distributed as dist
+    import cuzfp_amd as cz
+    from cuzfp_amd import dist as zd
+    from cuzfp_amd.datagen import polynomial_field
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        a = polynomial_field(shape, np.float32)
+        x = torch.from_numpy(a).to(dev)
+        words = cz.encode(x, maxbits)
+        full = zd.allgather_stream(words)
+        torch.cuda.synchronize()
+        q.put((dist.get_backend(), full.is_cuda, full.cpu().numpy().view(np.uint64).copy(),
+               words.cpu().numpy().view(np.uint64).copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(240)
+def test_rccl_one_rank_allgather(restatement):
+    """RCCL's library load, device binding and ncclAllGather run once on the
+    GPU box (verdict r04: the multi-GPU leg had never executed): one rank, the
+    gathered stream equals the local one and the reference's."""
+    import multiprocessing as mp
+    import torch
+    from cuzfp_amd.datagen import polynomial_field
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    shape, maxbits = (32, 48, 64), 512
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_one_rank_worker, args=(_free_port(), shape, maxbits, q))
+    p.start()
+    backend, on_gpu, full, local = q.get(timeout=200)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert backend == "nccl" and on_gpu
+    want = restatement.compress(polynomial_field(shape, np.float32), maxbits)
+    assert np.array_equal(local, want)
+    assert np.array_equal(full, want)
+
+
 def _config5_worker(rank, world, port, edge, q):
     # bench.py's configs[4] bookkeeping on CPU: StrongShard's slab and word
     # range, the oracle standing in for the kernels, the gloo all-gather, the

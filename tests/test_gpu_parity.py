@@ -7,6 +7,8 @@ the differential fuzz space of src/utils/test.py:101-132 (random dims, rates
 1..31, f32/f64) -- plus partial blocks, strides, integer fields and
 denormal / zero / huge-range blocks.
 """
+import zlib
+
 import numpy as np
 import pytest
 
@@ -63,7 +65,8 @@ def test_sanity_ramp(dims, dtype, cuda, restatement):
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 @pytest.mark.parametrize("kind", ["normal", "smooth", "range", "sparse"])
 def test_fuzz_vs_oracle(dims, dtype, kind, cuda, restatement):
-    rng = np.random.default_rng(hash((dims, np.dtype(dtype).str, kind)) & 0xffffffff)
+    # (a stable seed: hash() of a str is salted per process by PYTHONHASHSEED)
+    rng = np.random.default_rng(zlib.crc32(f"{dims}/{np.dtype(dtype).str}/{kind}".encode()))
     for trial in range(6):
         hi = {1: 400, 2: 100, 3: 24}[dims]
         shape = tuple(int(rng.integers(1, hi)) for _ in range(dims))
@@ -298,7 +301,7 @@ def test_random_streams(cuda, restatement, dims, dtype):
 @pytest.mark.parametrize("dims,shape", [(1, (3 * 2 ** 20 + 7,)), (2, (2050, 1030)), (1, (5 * 2 ** 20,))])
 @pytest.mark.parametrize("dtype", [np.float32, np.float64, np.int32])
 def test_persistent_batches(cuda, restatement, dims, shape, dtype):
-    rng = np.random.default_rng(hash((dims, shape, np.dtype(dtype).str)) % 2 ** 32)
+    rng = np.random.default_rng(zlib.crc32(f"{dims}/{shape}/{np.dtype(dtype).str}".encode()))
     if np.dtype(dtype).kind == "i":
         a = rng.integers(-2 ** 24, 2 ** 24, size=shape).astype(dtype)
     else:
@@ -434,6 +437,22 @@ def test_f64_staged_rows(cuda, restatement):
         ref = restatement.compress(a, mb)
         assert np.array_equal(words, ref), rate
         assert np.array_equal(y.view(np.uint8), restatement.decompress(ref, a.shape, np.float64, mb).view(np.uint8)), rate
+
+
+@pytest.mark.parametrize("dtype,mb", [(np.float32, 384), (np.float32, 640), (np.float64, 768), (np.float64, 1152)])
+def test_lane_order_non_pow2_words(cuda, restatement, dtype, mb):
+    """The full-wave lane-order stream copies (kernels.hpp: the encoder's
+    copy-out over W = maxbits/64 words a block, the decoder's copy-in over D =
+    maxbits/32 dwords) with W and D even but not powers of two, which takes
+    udivmod_uniform's division branch: 16 full 64-block waves of
+    a fixed-seed field, smooth and rough halves, against the restatement."""
+    rng = np.random.default_rng(384 + mb)
+    a = _fields(rng, (16, 16, 256), dtype, "smooth")
+    a[8:] = _fields(rng, (8, 16, 256), dtype, "normal")
+    words, y = _gpu_roundtrip(a, mb, cuda)
+    ref = restatement.compress(a, mb)
+    assert np.array_equal(words, ref), mb
+    assert np.array_equal(y.view(np.uint8), restatement.decompress(ref, a.shape, dtype, mb).view(np.uint8)), mb
 
 
 @pytest.mark.parametrize("nblocks", [64 * 32771, 64 * 32769 + 25, 64 * 32768 - 1])
