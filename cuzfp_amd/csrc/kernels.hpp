@@ -306,22 +306,25 @@ struct LdsReader {
         ((uint64_t)__builtin_amdgcn_alignbit(a2, a1, pos) << 32);
     g = __builtin_amdgcn_alignbit(b1, b0, q);
   }
-  // The fast plane step's windows, split so that the step waits on the LDS
-  // twice a plane rather than once per value (the compiler's own waits come
-  // before each first use): the group window m bits on, read and waited for
-  // alone (the step's critical path: its chunk lookups need it), then -- after
-  // the chunk lookups are issued -- the 64-bit window at the position, whose
-  // reads land in the lookups' shadow and are waited for with them.
-  __device__ __forceinline__ uint32_t window_g(uint32_t m) const {
+  // The fast plane step's windows: the group window m bits on (the step's
+  // critical path: its chunk lookups need it) and the 64-bit window at the
+  // position (needed only at the step's end).  Both are issued here, the
+  // group window's read first, and only it is waited for (lgkmcnt(2): the
+  // window's two reads may still be in flight); the window's dwords land in
+  // the lookups' shadow and window_w_make combines them after the step's one
+  // other wait.  (The compiler's own placement waits before each first use:
+  // six waits a plane.)
+  __device__ __forceinline__ uint32_t window_g(uint32_t m, WRaw& wr) const {
     const uint32_t q = pos + m;
     lds_u32* t = row(q);
     const uint32_t b0 = t[0], b1 = t[64];
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): vmcnt / expcnt not waited for
-    return __builtin_amdgcn_alignbit(b1, b0, q);
-  }
-  __device__ __forceinline__ WRaw window_w_issue() const {
+    __builtin_amdgcn_sched_barrier(0);
     lds_u32* r = row(pos);
-    return WRaw{r[0], r[64], r[128]};
+    wr = WRaw{r[0], r[64], r[128]};
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0xc27f);  // lgkmcnt(2); vmcnt / expcnt not waited for
+    __builtin_amdgcn_sched_barrier(0);
+    return __builtin_amdgcn_alignbit(b1, b0, q);
   }
   __device__ __forceinline__ uint64_t window_w_make(const WRaw& a) const {
     return (uint64_t)__builtin_amdgcn_alignbit(a.a1, a.a0, pos) | ((uint64_t)__builtin_amdgcn_alignbit(a.a2, a.a1, pos) << 32);
@@ -452,11 +455,11 @@ struct RegReader : LdsReader<PRIO> {
     else
       g = (uint32_t)at(this->pos + m);
   }
-  __device__ __forceinline__ uint32_t window_g(uint32_t m) const {
+  __device__ __forceinline__ uint32_t window_g(uint32_t m, WRaw& wr) const {
+    wr = WRaw{0u, 0u, 0u};
     if constexpr (B32) return (uint32_t)(blk4 >> (this->pos + m));  // the group window << 2
     return (uint32_t)at(this->pos + m);
   }
-  __device__ __forceinline__ WRaw window_w_issue() const { return WRaw{0u, 0u, 0u}; }
   __device__ __forceinline__ uint64_t window_w_make(const WRaw&) const { return at(this->pos); }
   // (B32: g from windows() is the group window << 2; its bit 2 is the leading
   // test)

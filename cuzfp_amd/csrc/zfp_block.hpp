@@ -415,7 +415,12 @@ ZFP_HD void transpose_stage(uint32_t* a, int rows) {
   // v_bfi_b32 per output word: 3 instructions a pair instead of 4
   constexpr uint32_t m = J == 16 ? 0x0000ffffu : J == 8 ? 0x00ff00ffu : J == 4 ? 0x0f0f0f0fu
                        : J == 2 ? 0x33333333u : 0x55555555u;
-  if constexpr (J <= 4) {
+#if defined(CUZFP_EXP_T32)
+  constexpr bool kPairs64 = false;  // A/B builds: the 32-bit shifts
+#else
+  constexpr bool kPairs64 = true;
+#endif
+  if constexpr (J <= 4 && kPairs64) {
     // the partner pair: i + 1 for J >= 2 (adjacent words), i + 2 for J = 1
     constexpr int D = J == 1 ? 2 : 1;
     const uint32_t sj = opaque_shift<J>();
@@ -885,9 +890,11 @@ ZFP_HD void encode_plane_one_put(PW x, unsigned nf, uint64_t r, const PlaneLen& 
   // each before its first use: two s_waitcnt a plane)
   const uint32_t e0 = wr.sp0(byte_off4<0>(rl));
   const uint32_t e1 = N > 4 ? wr.sp1(byte_off4<1>(rl)) : 0u;
+#if !defined(CUZFP_EXP_EWAIT_OLD)  // (A/B builds: the compiler's two waits)
   sched_fence();
   wr.lds_wait();
   sched_fence();
+#endif
   uint32_t G = e0 >> 5;
   if constexpr (N > 4) G |= e1 << (e0 & 31u);
   const uint32_t g = low_bits(G, width);
@@ -1726,17 +1733,28 @@ ZFP_HD PW decode_plane_fast_any(unsigned& n, Reader& rd) {
   const unsigned nf = n;  // <= N-1
   // the group window first (the lookups wait on it), the verbatim window's
   // reads after the lookups' (Reader::window_g / window_w)
-  const uint32_t g = rd.window_g(nf);
+#if defined(CUZFP_EXP_DWAIT_OLD)  // A/B builds: the compiler's waits
+  uint64_t w;
+  uint32_t g;
+  rd.windows(nf, w, g);
+  uint32_t e1, e2, e2a = 0, e2b = 0;
+  if constexpr (DIMS == 1)
+    e1 = rd.chunk1_fast(g);
+  else
+    rd.chunks_fast(g, e1, e2a, e2b);
+#else
+  WRaw wr;
+  const uint32_t g = rd.window_g(nf, wr);
   uint32_t e1, e2, e2a = 0, e2b = 0;
   if constexpr (DIMS == 1)
     e1 = rd.chunk1_fast(g);  // a 1D code fits chunk 1
   else
     rd.chunks_fast(g, e1, e2a, e2b);
-  const WRaw wr = rd.window_w_issue();
   sched_fence();
-  rd.lds_wait();  // one wait for the lookups and the window
+  rd.lds_wait();  // one wait for the lookups (and the window's dwords)
   sched_fence();
   const uint64_t w = rd.window_w_make(wr);
+#endif
   if constexpr (DIMS == 1) {
     e2 = 0;
   } else {
@@ -2224,9 +2242,14 @@ ZFP_HD bool decode_block(Scalar* f, unsigned maxbits, Reader& rd) {
     // A wave of zero blocks returns at once.
     if (!any_lane(coded)) return false;
     emax = (int)((head >> 1) & lowmask(T::ebits)) - T::ebias;
+    const auto start = rd.pos;
     rd.skip(T::ebits + 1);
     maxprec = precision<DIMS>(emax, T::prec);
     budget = coded ? maxbits - (T::ebits + 1) : 0u;
+    // (the plane steps take the stream as zeros past the budget's end, which
+    // a zero block's bits need not be: its reads start at the block's end,
+    // where the readers hold zeros)
+    if (!coded) rd.pos = start + maxbits;
   }
   UInt u[N];
 #if defined(CUZFP_PROBE) && CUZFP_PROBE == 2

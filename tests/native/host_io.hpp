@@ -80,13 +80,13 @@ struct HostReader {
     g = (uint32_t)peek();
     pos -= m;
   }
-  uint32_t window_g(unsigned m) {
+  uint32_t window_g(unsigned m, cuzfp::WRaw& wr) {
+    wr = cuzfp::WRaw{0u, 0u, 0u};
     pos += m;
     const uint32_t g = (uint32_t)peek();
     pos -= m;
     return g;
   }
-  cuzfp::WRaw window_w_issue() const { return cuzfp::WRaw{0u, 0u, 0u}; }
   uint64_t window_w_make(const cuzfp::WRaw&) const { return peek(); }
   void lds_wait() const {}
   // the 1D plane table (o: byte offset) and the next 8 stream bits

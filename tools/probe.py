@@ -113,8 +113,8 @@ print("ok")
 """
 
 
-def stamps(size, field, outdir, back=1, dims=3, rate=8.0, dtype="float32"):
-    lib = os.path.join(OUT, "p9", "libcuzfp_hip.so")
+def stamps(size, field, outdir, back=1, dims=3, rate=8.0, dtype="float32", variant="p9"):
+    lib = os.path.join(OUT, variant, "libcuzfp_hip.so")
     code = STAMP_CODE.replace("@ROOT@", repr(ROOT)).replace("@LIB@", repr(lib)).replace("@SIZE@", str(size)) \
         .replace("@FIELD@", repr(field)).replace("@OUTDIR@", repr(outdir)).replace("@BACK@", str(back)) \
         .replace("@SHAPE@", _shape(size, dims)).replace("@DIMS@", str(dims)).replace("@RATE@", str(rate)) \
@@ -167,12 +167,13 @@ if __name__ == "__main__":
     ap.add_argument("--dims", type=int, default=3)
     ap.add_argument("--rate", type=float, default=8.0)
     ap.add_argument("--dtype", default="float32")
+    ap.add_argument("--lib", default="p9", help="stamps: the build/probe/ subdirectory of the stamped library")
     a = ap.parse_args()
     if a.cmd == "build":
         build(tuple(int(v) for v in a.variants.split(",")))
     elif a.cmd == "stamps":
         od = os.path.join(ROOT, "gpurun_out")
         os.makedirs(od, exist_ok=True)
-        stamps(a.size, a.field, od, a.back, a.dims, a.rate, a.dtype)
+        stamps(a.size, a.field, od, a.back, a.dims, a.rate, a.dtype, a.lib)
     else:
         run(a.size, a.field, a.dims, a.rate, dtype=a.dtype)

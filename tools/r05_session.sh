@@ -24,6 +24,13 @@ for s in "$@"; do
       IFS=: read -r _ names <<< "$s"
       timeout -k 10 600 python tools/xvar.py run --dtype float64 --rate 16 ${names//,/ } > "$OUT/xvar64_${TAG}.txt" 2>&1
       stop_on $? xvar64; cat "$OUT/xvar64_${TAG}.txt" ;;
+    hostsweep)
+      timeout -k 10 300 python tools/host_sweep.py > "$OUT/host_sweep_${TAG}.txt" 2>&1
+      stop_on $? hostsweep; cat "$OUT/host_sweep_${TAG}.txt" ;;
+    stamps:*)  # stamps:LIB[:field] -- build/probe/LIB, 3D f32 256^3 r8, two launches back to back
+      IFS=: read -r _ lib field <<< "$s"
+      timeout -k 10 300 python tools/probe.py stamps --lib $lib --field ${field:-polynomial} --back 2 > "$OUT/stamps_${lib}_${TAG}.txt" 2>&1
+      stop_on $? stamps; cat "$OUT/stamps_${lib}_${TAG}.txt" ;;
     launch)
       timeout -k 10 300 python tools/launch_overhead.py > "$OUT/launch_${TAG}.txt" 2>&1
       stop_on $? launch; cat "$OUT/launch_${TAG}.txt" ;;
@@ -31,6 +38,11 @@ for s in "$@"; do
       timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread \
         -k "golden_baseline or fuzz_vs_oracle or extreme or random_streams or golden_fuzz or non_pow2 or sanity or edge_sizes or staged" > "$OUT/pytest_quick_${TAG}.log" 2>&1
       stop_on $? quick; tail -3 "$OUT/pytest_quick_${TAG}.log" ;;
+    pytestk:*)  # pytestk:EXPR -- the GPU tests matching EXPR
+      IFS=: read -r _ expr <<< "$s"
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread \
+        -k "$expr" > "$OUT/pytestk_${TAG}.log" 2>&1
+      stop_on $? pytestk; tail -3 "$OUT/pytestk_${TAG}.log" ;;
     pytest)
       timeout -k 10 1500 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > "$OUT/pytest_gpu_${TAG}.log" 2>&1
       stop_on $? pytest; tail -3 "$OUT/pytest_gpu_${TAG}.log" ;;
