@@ -759,7 +759,9 @@ def main():
                          "link_GBps": {"h2d": round(h2d, 2), "d2h": round(d2h, 2)},
                          "frac_of_link": {"compress": round(n_in / tc / 1e9 / c_link, 3),
                                           "decompress": round(n_in / td / 1e9 / c_link, 3)},
-                         "chunk_bytes": int(os.environ.get("CUZFP_HOST_CHUNK_BYTES", 8 << 20)), "nstreams": 4,
+                         "chunk_bytes": int(os.environ.get("CUZFP_HOST_CHUNK_BYTES", 64 << 20)), "nstreams": 4,
+                         "schedule": "per-stream" if os.environ.get("CUZFP_HOST_ORDERED", "1") == "0" else "ordered",
+                         "zero_copy": int(os.environ.get("CUZFP_HOST_ZEROCOPY", "0") or 0),
                          "note": "pinned host buffers, PCIe-inclusive (cuzfp_hip_compress_host/decompress_host); "
                                  "frac_of_link = rate / (input bytes / max(input/h2d, stream/d2h)), the "
                                  "full-duplex bound"}

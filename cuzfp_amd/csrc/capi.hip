@@ -100,21 +100,61 @@ static uint32_t waves_of(const Geometry& g) { return (g.nblocks + kLanes - 1) / 
 // Pinned (hipHostMalloc / registered) user buffers are DMA'd in place;
 // pageable ones go through a ring of pinned staging buffers.
 
-// 8 MiB chunks on 4 streams: tools/host_sweep.py (profiles/r02_host_sweep.txt),
-// 256^3 f32 rate 8 from pinned buffers: 43-46 GB/s each way against a 52.6 /
-// 55.0 GB/s pinned H2D / D2H link; 32 MiB on 2 streams 43 GB/s; 1 stream
-// 21-43 GB/s; 2-4 MiB chunks 32-47 GB/s, noisier.
-constexpr size_t kChunkBytes = 8u << 20;
+// Chunk size: 64 MiB between pinned buffers (ordered schedule, 256^3 f32
+// rate 8: compression 50.4 GB/s, decompression 48.9 against a 54.8 / 55.3 GB/s
+// link; 32 MiB 49.7 / 48.1, 16 MiB 49.0 / 47.3; the round-4 schedule at 8 MiB
+// 44.1 / 47.4: tools/host_sweep.py, profiles/r05_host_sweep.txt).  Pageable
+// buffers go through pinned staging buffers a chunk each, bound by the host
+// copies into them: 8 MiB keeps that staging small.
+constexpr size_t kChunkBytes = 64u << 20, kStagedChunkBytes = 8u << 20;
 
-// chunk size: kChunkBytes, or CUZFP_HOST_CHUNK_BYTES from the environment
+// chunk size: the above, or CUZFP_HOST_CHUNK_BYTES from the environment
 // (read per call; tests use small chunks to run the multi-chunk paths)
-static size_t chunk_bytes() {
+static size_t chunk_bytes(bool staged) {
   const char* e = getenv("CUZFP_HOST_CHUNK_BYTES");
   if (e && *e) {
     const long long v = atoll(e);
     if (v > 0) return (size_t)v;
   }
-  return kChunkBytes;
+  return staged ? kStagedChunkBytes : kChunkBytes;
+}
+
+// schedule: ordered copy queues (host_pipeline); CUZFP_HOST_ORDERED=0 -> the
+// round-4 schedule, chunk i's copies and kernel on stream i % S (tests run both)
+static bool host_ordered() {
+  const char* e = getenv("CUZFP_HOST_ORDERED");
+  return !(e && *e == '0');
+}
+
+// Zero-copy level (CUZFP_HOST_ZEROCOPY, opt-in): 0 (default) none; 1:
+// compression of a pinned array into a pinned stream is one encode launch that
+// loads the array and stores the stream over PCIe itself; 2: also
+// decompression into a pinned array, the decode kernels storing to it (the
+// stream still copied in chunks).  256^3 f32 rate 8 (tools/zero_copy.py,
+// tools/host_sweep.py, profiles/r05_host_sweep.txt): compression 50.2 GB/s
+// against 50.4 for the copy pipeline, decompression 42.3 against 48.9 -- the
+// kernels' own PCIe stores reach 49.6 GB/s (53.1 for a plain copy kernel)
+// where the copy engine reaches 55.
+static int host_zero_copy() {
+  const char* e = getenv("CUZFP_HOST_ZEROCOPY");
+  return (e && *e) ? atoi(e) : 0;
+}
+
+// The device address of [p, p + bytes) when the whole range lies in one pinned
+// host allocation mapped into the device's address space (hipHostMalloc, a
+// pinned torch tensor), else null.  Registered memory reports no allocation
+// base (hipMemGetAddressRange; tools/zero_copy.py --ranges) and is not used.
+static char* mapped_view(const void* p, size_t bytes) {
+  hipPointerAttribute_t a;
+  void* d = nullptr;
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  const bool ok = hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeHost &&
+                  hipHostGetDevicePointer(&d, const_cast<void*>(p), 0) == hipSuccess && d &&
+                  hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)d) == hipSuccess && base &&
+                  (char*)d >= (char*)base && (size_t)((char*)d - (char*)base) + bytes <= size;
+  (void)hipGetLastError();
+  return ok ? (char*)d : nullptr;
 }
 
 static bool is_pinned_host(const void* ptr) {
@@ -254,17 +294,47 @@ static int host_pipeline(const Problem& p, bool encode, void* h_data, void* h_st
   const size_t data_bytes = total_vals * es;
   const size_t sbytes = stream_bytes_of(g);
   const size_t wave_bytes = (size_t)g.maxbits * 8;  // stream bytes per full wave
-  const size_t per = std::max<size_t>(1, chunk_bytes() / (slab_vals * es));
+  const bool data_pinned = is_pinned_host(h_data);
+  const bool stream_pinned = is_pinned_host(h_stream);
+  const size_t per = std::max<size_t>(1, chunk_bytes(!data_pinned || !stream_pinned) / (slab_vals * es));
 
+  const bool ordered = host_ordered();
+  // chunk lengths in slabs: `per` each, except (ordered schedule) at the
+  // pipeline's exposed end -- the last chunks of a compression, whose kernels
+  // and stream copies trail the input copies, and the first of a
+  // decompression, before whose kernel no output copy can start -- which grow
+  // by 3x from about nslabs / 32 (256^3 f32, 1 MiB slabs, at 32 MiB chunks:
+  // compression 19, 19, 18, 6, 2 slabs; decompression 2, 6, 18, 19, 19).  The stream is a
+  // quarter of the data or less, so chunk i + 1's stream copy and kernel
+  // finish within chunk i's data copy at 3x growth, and the copy queue that
+  // binds never waits; every copy also costs ~10-15 us of its own
+  // (tools/copy_chunks.py), so the chunks stay few.
+  std::vector<size_t> lens;
+  {
+    std::vector<size_t> edge;  // from the exposed end inward
+    size_t sum = 0;
+    if (ordered) {
+      for (size_t l = std::max<size_t>(1, nslabs / 32); sum + l < nslabs && l < per; l *= 3) {
+        edge.push_back(l);
+        sum += l;
+      }
+    }
+    // the rest in equal chunks of at most `per`
+    const size_t body = nslabs - sum, nb = (body + per - 1) / per;
+    if (!encode) lens = edge;
+    for (size_t k = 0; k < nb; k++) lens.push_back(body / nb + (k < body % nb ? 1 : 0));
+    if (encode) lens.insert(lens.end(), edge.rbegin(), edge.rend());
+  }
   std::vector<Chunk> chunks;
   uint32_t w_prev = 0;
   size_t d_prev = 0;
-  for (size_t s = 0; s < nslabs; s += per) {
-    const size_t e = std::min(nslabs, s + per);
+  size_t sl = 0;  // first slab of the chunk
+  for (size_t len : lens) {
+    const size_t e = sl + len;
     const bool last = e == nslabs;
     Chunk c;
     if (encode) {
-      c.d0 = std::min(data_bytes, s * slab_vals * es);
+      c.d0 = std::min(data_bytes, sl * slab_vals * es);
       c.d1 = last ? data_bytes : e * slab_vals * es;
       c.w0 = w_prev;
       c.w1 = last ? nwaves : (uint32_t)(e * slab_blocks / kLanes);
@@ -281,19 +351,30 @@ static int host_pipeline(const Problem& p, bool encode, void* h_data, void* h_st
     c.s0 = std::min(sbytes, (size_t)c.w0 * wave_bytes);
     c.s1 = last ? sbytes : std::min(sbytes, (size_t)c.w1 * wave_bytes);
     chunks.push_back(c);
+    sl = e;
   }
 
   const int S = std::max(1, std::min(nstreams, kMaxStreams));
-  const bool data_pinned = is_pinned_host(h_data);
-  const bool stream_pinned = is_pinned_host(h_stream);
   int dev = 0;
   CUZFP_HIP_TRY(hipGetDevice(&dev));
   if (dev < 0 || dev >= kMaxDevices) return CUZFP_ERROR_INVALID_ARGUMENT;
   PipelineCache& r = g_pipeline[dev];
   std::lock_guard<std::mutex> lock(r.mu);
+  // zero-copy views (host_zero_copy): both buffers for a compression, the
+  // array for a decompression (ordered schedule)
+  const int zc = host_zero_copy();
+  char* in_view = nullptr;
+  char* out_view = nullptr;
+  if (encode && zc >= 1) {
+    in_view = mapped_view(h_data, data_bytes);
+    out_view = in_view ? mapped_view(h_stream, sbytes) : nullptr;
+    if (!out_view) in_view = nullptr;
+  } else if (!encode && zc >= 2 && ordered) {
+    out_view = mapped_view(h_data, data_bytes);
+  }
   CallBuf bd, bs;
-  CUZFP_HIP_TRY(bd.get(r.d_data, data_bytes));
-  CUZFP_HIP_TRY(bs.get(r.d_stream, sbytes));
+  if (!out_view) CUZFP_HIP_TRY(bd.get(r.d_data, data_bytes));
+  if (!in_view) CUZFP_HIP_TRY(bs.get(r.d_stream, sbytes));
   size_t max_in = 0, max_out = 0;
   for (const Chunk& c : chunks) {
     max_in = std::max(max_in, encode ? c.d1 - c.d0 : c.s1 - c.s0);
@@ -301,7 +382,9 @@ static int host_pipeline(const Problem& p, bool encode, void* h_data, void* h_st
   }
   const bool in_pinned = encode ? data_pinned : stream_pinned;
   const bool out_pinned = encode ? stream_pinned : data_pinned;
-  for (int i = r.nst; i < S; i++) {
+  // the ordered schedule uses three streams whatever S is
+  const int NS = ordered ? std::max(S, 3) : S;
+  for (int i = r.nst; i < NS; i++) {
     CUZFP_HIP_TRY(hipStreamCreateWithFlags(&r.st[i], hipStreamNonBlocking));
     CUZFP_HIP_TRY(hipEventCreateWithFlags(&r.ev_in[i], hipEventDisableTiming));
     CUZFP_HIP_TRY(hipEventCreateWithFlags(&r.ev_kernel[i], hipEventDisableTiming));
@@ -322,7 +405,7 @@ static int host_pipeline(const Problem& p, bool encode, void* h_data, void* h_st
     ~Drain() {
       for (int i = 0; i < S; i++) (void)hipStreamSynchronize(r.st[i]);
     }
-  } drain{r, S};
+  } drain{r, NS};
   char* hd = (char*)h_data;
   char* hs = (char*)h_stream;
   char* dd = (char*)bd.p;
@@ -332,6 +415,63 @@ static int host_pipeline(const Problem& p, bool encode, void* h_data, void* h_st
     *o1 = encode ? c.s1 : c.d1;
   };
   const size_t n = chunks.size();
+  if (in_view) {
+    // one launch over the whole array: its loads of the pinned array and
+    // stores of the pinned stream cross PCIe as the waves run
+    return launch_encode(p, in_view, (uint64_t*)out_view, 0, nwaves, r.st[0]);  // Drain waits for it
+  }
+  if (ordered) {
+    // three queues, each in chunk order: input copies on st[0], kernels on
+    // st[1], output copies on st[2].  Chunk i's input lands at (i + 1) input
+    // copies' time, so its kernel and output copy start then, and only the
+    // last chunk's kernel and output copy trail the input stream.  Slots
+    // (i % S) only matter for the pinned staging buffers: a slot is reused
+    // once its previous chunk's copies are done.
+    hipStream_t sin = r.st[0], sk = r.st[1], sout = r.st[2];
+    for (size_t i = 0; i < n + S; i++) {
+      if (i >= (size_t)S) {
+        const size_t j = i - S;
+        const int sj = (int)(j % S);
+        if (!out_pinned) {
+          CUZFP_HIP_TRY(hipEventSynchronize(r.ev_done[sj]));
+          size_t o0, o1;
+          out_range(chunks[j], &o0, &o1);
+          if (o1 > o0) std::memcpy((encode ? hs : hd) + o0, pin_out[sj].p, o1 - o0);
+        } else if (!in_pinned) {
+          CUZFP_HIP_TRY(hipEventSynchronize(r.ev_in[sj]));
+        }
+      }
+      if (i >= n) continue;
+      const Chunk& c = chunks[i];
+      const int s = (int)(i % S);
+      const size_t i0 = encode ? c.d0 : c.s0, i1 = encode ? c.d1 : c.s1;
+      char* src = (encode ? hd : hs) + i0;
+      if (i1 > i0) {
+        if (!in_pinned) {
+          std::memcpy(pin_in[s].p, src, i1 - i0);
+          src = (char*)pin_in[s].p;
+        }
+        CUZFP_HIP_TRY(hipMemcpyAsync((encode ? dd : ds) + i0, src, i1 - i0, hipMemcpyHostToDevice, sin));
+      }
+      CUZFP_HIP_TRY(hipEventRecord(r.ev_in[s], sin));
+      // every earlier chunk's input (encode) / kernel (decode) is ahead of
+      // this one in its queue, so one wait covers the straddling waves
+      CUZFP_HIP_TRY(hipStreamWaitEvent(sk, r.ev_in[s], 0));
+      int rc = encode ? launch_encode(p, dd, (uint64_t*)ds, c.w0, c.w1 - c.w0, sk)
+                      : launch_decode(p, (const uint64_t*)ds, out_view ? out_view : dd, c.w0, c.w1 - c.w0, sk);
+      if (rc) return rc;
+      CUZFP_HIP_TRY(hipEventRecord(r.ev_kernel[s], sk));
+      if (out_view) continue;  // the kernel stored its blocks to the pinned array itself
+      CUZFP_HIP_TRY(hipStreamWaitEvent(sout, r.ev_kernel[s], 0));
+      size_t o0, o1;
+      out_range(c, &o0, &o1);
+      if (o1 > o0)
+        CUZFP_HIP_TRY(hipMemcpyAsync(out_pinned ? (encode ? hs : hd) + o0 : (char*)pin_out[s].p,
+                                     (encode ? ds : dd) + o0, o1 - o0, hipMemcpyDeviceToHost, sout));
+      CUZFP_HIP_TRY(hipEventRecord(r.ev_done[s], sout));
+    }
+    return CUZFP_SUCCESS;
+  }
   for (size_t i = 0; i < n + S; i++) {
     // retire chunk i - S: its slot's buffers become free
     if (i >= (size_t)S) {

@@ -69,8 +69,8 @@ extern "C" {
  * CUZFP_LDS_CAP_BYTES lowers the budget (tests). */
 #define CUZFP_MAX_BITS 16384
 
-/* Streams the host-memory pipeline is measured best with (callers' default
- * `nstreams` for cuzfp_hip_compress_host / decompress_host). */
+/* Pinned staging slots of the host-memory pipeline for pageable buffers
+ * (callers' default `nstreams` for cuzfp_hip_compress_host / decompress_host). */
 #define CUZFP_HOST_STREAMS 4
 
 typedef enum {
@@ -112,17 +112,24 @@ int cuzfp_hip_decode(const uint64_t* d_stream, size_t stream_bytes, int type, un
                      unsigned maxbits, void* d_data, hipStream_t stream);
 
 /* Host-memory end to end: the array and the stream live in
- * host memory; the library moves them through pinned staging buffers in
- * z-slab (3D) / y-slab (2D) / x-range (1D) chunks on `nstreams` HIP streams so
- * the copies overlap the kernels.  Synchronous; contiguous arrays only.
+ * host memory; the library moves them in z-slab (3D) / y-slab (2D) / x-range
+ * (1D) chunks on three HIP streams -- input copies, kernels, output copies,
+ * each in chunk order -- so the copies overlap the kernels and each other
+ * (64 MiB chunks between pinned buffers, smaller ones at the pipeline's ends;
+ * 8 MiB through `nstreams` pinned staging buffers for pageable ones).
+ * Synchronous; contiguous arrays only.  Environment (read per call):
+ * CUZFP_HOST_CHUNK_BYTES sets the chunk size, CUZFP_HOST_ORDERED=0 selects
+ * round 4's schedule (chunk i's copies and kernel on stream i % nstreams),
+ * CUZFP_HOST_ZEROCOPY=1/2 lets the kernels load / store pinned buffers
+ * directly (opt-in; capi.hip host_zero_copy has the measurements).
  *
  * Retention: the first call on a device allocates, and keeps for later calls,
  * device buffers for the array and the stream (grown to the largest call, up
- * to 1 GiB each; larger calls use buffers freed on return), `nstreams` HIP
- * streams with their events, and (for pageable user buffers) pinned staging
- * buffers of one chunk each (at most 64 MiB apiece).  This memory is outside
- * any framework allocator (e.g. torch's caching allocator).  Calls on one
- * device are serialised; calls on different devices run concurrently. */
+ * to 1 GiB each; larger calls use buffers freed on return), its HIP streams
+ * with their events, and (for pageable user buffers) pinned staging buffers of
+ * one chunk each (at most 64 MiB apiece).  This memory is outside any
+ * framework allocator (e.g. torch's caching allocator).  Calls on one device
+ * are serialised; calls on different devices run concurrently. */
 int cuzfp_hip_compress_host(const void* h_data, int type, unsigned nx, unsigned ny,
                             unsigned nz, unsigned maxbits, void* h_stream,
                             size_t stream_capacity, size_t* out_bytes, int nstreams);

@@ -266,6 +266,36 @@ def test_host_pipeline(cuda, restatement, shape, dtype, rate, pinned):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("zero_copy", ["1", "2"])
+def test_host_zero_copy_views(cuda, restatement, monkeypatch, zero_copy):
+    """Zero-copy host paths on pinned buffers that are views inside larger
+    pinned allocations (offset starts, a stream buffer larger than the stream):
+    byte-equal to the oracle, and the bytes around the views untouched."""
+    import torch
+    from cuzfp_amd.datagen import splitmix_uniform
+    monkeypatch.setenv("CUZFP_HOST_ZEROCOPY", zero_copy)
+    shape, dtype, mb = (40, 36, 28), np.float32, cz.rate_to_maxbits(8, np.float32, 3)
+    a = splitmix_uniform(shape, dtype, seed=11)
+    n = a.size
+    big = torch.zeros(n + 64, dtype=torch.float32).pin_memory().numpy()
+    big[16:16 + n] = a.ravel()
+    view = big[16:16 + n].reshape(shape)
+    nw = cz.stream_bytes(shape, dtype, mb) // 8
+    sbig = torch.full((nw + 40,), -1, dtype=torch.int64).pin_memory().numpy().view(np.uint64)
+    sview = sbig[8:8 + nw + 16]  # capacity beyond the stream
+    ref = restatement.compress(a, mb)
+    want = restatement.decompress(ref, shape, dtype, mb)
+    s = cz.compress_host(view, mb, out=sview)[:nw]
+    assert np.array_equal(s, ref)
+    assert np.all(sbig[:8] == np.uint64(2**64 - 1)) and np.all(sbig[8 + nw:] == np.uint64(2**64 - 1))
+    ybig = torch.full((n + 64,), 7.0, dtype=torch.float32).pin_memory().numpy()
+    yview = ybig[32:32 + n].reshape(shape)
+    y = cz.decompress_host(s, shape, dtype, mb, out=yview)
+    assert np.array_equal(y.view(np.uint32), want.view(np.uint32))
+    assert np.all(ybig[:32] == 7.0) and np.all(ybig[32 + n:] == 7.0)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("dims", [1, 2, 3])
 @pytest.mark.parametrize("dtype", [np.float32, np.float64, np.int32, np.int64])
 def test_random_streams(cuda, restatement, dims, dtype):
@@ -476,11 +506,17 @@ def test_batched_1d_waves(cuda, restatement, nblocks, dtype):
 @pytest.mark.parametrize("shape,dtype,rate", [((64, 48, 40), np.float32, 8), ((24, 20, 16), np.float64, 16),
                                               ((300, 260), np.float32, 4), ((200003,), np.float32, 8)])
 @pytest.mark.parametrize("pinned", [False, True])
-def test_host_pipeline_multi_chunk(cuda, restatement, monkeypatch, shape, dtype, rate, pinned):
+@pytest.mark.parametrize("ordered,zero_copy", [("0", "0"), ("1", "0"), ("1", "2")])
+def test_host_pipeline_multi_chunk(cuda, restatement, monkeypatch, shape, dtype, rate, pinned, ordered, zero_copy):
     """The host pipeline with chunks far smaller than the array
     (CUZFP_HOST_CHUNK_BYTES): waves straddling chunks, the cross-stream event
-    waits and the pageable staging ring, for 1, 2 and 3 streams."""
+    waits and the pageable staging ring, for 1, 2 and 3 streams, in both
+    schedules (CUZFP_HOST_ORDERED), with the kernels addressing pinned buffers
+    themselves (CUZFP_HOST_ZEROCOPY=2: compression in one launch, decode
+    kernels storing to the array) or not (0)."""
     import torch
+    monkeypatch.setenv("CUZFP_HOST_ORDERED", ordered)
+    monkeypatch.setenv("CUZFP_HOST_ZEROCOPY", zero_copy)
     from cuzfp_amd.datagen import splitmix_uniform
     a = splitmix_uniform(shape, dtype, seed=9)
     mb = cz.rate_to_maxbits(rate, dtype, len(shape))
@@ -491,7 +527,9 @@ def test_host_pipeline_multi_chunk(cuda, restatement, monkeypatch, shape, dtype,
         a = torch.from_numpy(a).pin_memory().numpy()
         out = torch.empty(cz.stream_bytes(shape, dtype, mb) // 8, dtype=torch.int64).pin_memory().numpy().view(np.uint64)
     slab = a.nbytes // (shape[0] // 4 if len(shape) > 1 else max(1, shape[0] // 4))
-    for chunk in (1, 3 * slab + 5, a.nbytes // 7):
+    # 8 slabs a chunk and a.nbytes // 7 (1D, 2D) run the ordered schedule's
+    # halving edge chunks (capi.hip host_pipeline)
+    for chunk in (1, 3 * slab + 5, 8 * slab, a.nbytes // 7):
         monkeypatch.setenv("CUZFP_HOST_CHUNK_BYTES", str(chunk))
         for nstreams in (1, 2, 3):
             s = cz.compress_host(a, mb, nstreams=nstreams, out=out)

@@ -24,7 +24,7 @@ sys.path.insert(0, ROOT)
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--size", type=int, default=256)
-    p.add_argument("--reps", type=int, default=5)
+    p.add_argument("--reps", type=int, default=9)
     a = p.parse_args()
     import torch
     import cuzfp_amd as cz
@@ -41,23 +41,33 @@ def main():
     def rate(fn, n):
         fn()
         torch.cuda.synchronize()
-        t = time.perf_counter()
+        ts = []
         for _ in range(a.reps):
+            t = time.perf_counter()
             fn()
-        torch.cuda.synchronize()
-        return round(n / ((time.perf_counter() - t) / a.reps) / 1e9, 2)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t)
+        ts.sort()
+        return round(n / ts[len(ts) // 2] / 1e9, 2)
 
     res = {"h2d_GBps": rate(lambda: d.copy_(h_in, non_blocking=True), arr.nbytes),
            "d2h_GBps": rate(lambda: h_s.copy_(ds, non_blocking=True), nbytes), "runs": []}
     print(json.dumps({k: v for k, v in res.items() if k != "runs"}), flush=True)
     s_np = h_s.numpy().view(np.uint64)
-    for chunk_mb in (2, 4, 8, 16, 32, 64):
-        os.environ["CUZFP_HOST_CHUNK_BYTES"] = str(chunk_mb << 20)
-        for ns in (1, 2, 3, 4):
+    d.copy_(h_in)
+    want = cz.decode(cz.encode(d, mb), arr.shape, d.dtype, mb).cpu().numpy().view(np.uint32)
+    for zc, ordered, chunks in (("0", "0", (8,)), ("0", "1", (16, 32, 64)), ("1", "1", (32,))):
+        os.environ["CUZFP_HOST_ZEROCOPY"] = zc
+        os.environ["CUZFP_HOST_ORDERED"] = ordered
+        for chunk_mb in chunks:
+            os.environ["CUZFP_HOST_CHUNK_BYTES"] = str(chunk_mb << 20)
+            ns = 4
             c = rate(lambda: cz.compress_host(h_in.numpy(), mb, nstreams=ns, out=s_np), arr.nbytes)
             dcp = rate(lambda: cz.decompress_host(s_np, arr.shape, np.float32, mb, nstreams=ns, out=h_out.numpy()),
                        arr.nbytes)
-            r = {"chunk_MiB": chunk_mb, "nstreams": ns, "compress_GBps": c, "decompress_GBps": dcp}
+            ok = bool(np.array_equal(h_out.numpy().view(np.uint32), want))
+            r = {"zero_copy": zc, "ordered": ordered, "chunk_MiB": chunk_mb, "nstreams": ns, "compress_GBps": c,
+                 "decompress_GBps": dcp, "roundtrip_equal": ok}
             res["runs"].append(r)
             print(json.dumps(r), flush=True)
     best = max(res["runs"], key=lambda r: r["compress_GBps"] + r["decompress_GBps"])

@@ -31,6 +31,15 @@ for s in "$@"; do
       IFS=: read -r _ lib field <<< "$s"
       timeout -k 10 300 python tools/probe.py stamps --lib $lib --field ${field:-polynomial} --back 2 > "$OUT/stamps_${lib}_${TAG}.txt" 2>&1
       stop_on $? stamps; cat "$OUT/stamps_${lib}_${TAG}.txt" ;;
+    copychunks)
+      timeout -k 10 300 python tools/copy_chunks.py > "$OUT/copy_chunks_${TAG}.txt" 2>&1
+      stop_on $? copychunks; cat "$OUT/copy_chunks_${TAG}.txt" ;;
+    ranges)
+      timeout -k 10 120 python tools/zero_copy.py --ranges > "$OUT/ranges_${TAG}.txt" 2>&1
+      stop_on $? ranges; cat "$OUT/ranges_${TAG}.txt" ;;
+    zerocopy)
+      timeout -k 10 300 python tools/zero_copy.py > "$OUT/zero_copy_${TAG}.txt" 2>&1
+      stop_on $? zerocopy; cat "$OUT/zero_copy_${TAG}.txt" ;;
     launch)
       timeout -k 10 300 python tools/launch_overhead.py > "$OUT/launch_${TAG}.txt" 2>&1
       stop_on $? launch; cat "$OUT/launch_${TAG}.txt" ;;
