@@ -2234,6 +2234,9 @@ ZFP_HD bool decode_block(Scalar* f, unsigned maxbits, Reader& rd) {
     // decode.c:352-381
     const uint64_t head = rd.peek();
     const bool coded = head & 1;
+#if defined(CUZFP_EXP_ZB_LANE)  // A/B builds: round 4's per-lane return of a zero block
+    if (!coded) return false;
+#endif
     // A zero block (decode.c:354-355) takes the coded path with no budget
     // inside a wave that holds coded blocks: it reads no planes, so its q
     // are zero and its values 0 * 2^(emax-p+2) = +0 whatever its header bits
