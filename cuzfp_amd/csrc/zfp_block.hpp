@@ -415,12 +415,7 @@ ZFP_HD void transpose_stage(uint32_t* a, int rows) {
   // v_bfi_b32 per output word: 3 instructions a pair instead of 4
   constexpr uint32_t m = J == 16 ? 0x0000ffffu : J == 8 ? 0x00ff00ffu : J == 4 ? 0x0f0f0f0fu
                        : J == 2 ? 0x33333333u : 0x55555555u;
-#if defined(CUZFP_EXP_T32)
-  constexpr bool kPairs64 = false;  // A/B builds: the 32-bit shifts
-#else
-  constexpr bool kPairs64 = true;
-#endif
-  if constexpr (J <= 4 && kPairs64) {
+  if constexpr (J <= 4) {
     // the partner pair: i + 1 for J >= 2 (adjacent words), i + 2 for J = 1
     constexpr int D = J == 1 ? 2 : 1;
     const uint32_t sj = opaque_shift<J>();
@@ -673,11 +668,16 @@ ZFP_HD bool any_lane(bool p) {
 // alone at the end, at a fraction of the SIMD's issue rate).
 //
 // The encoder drops to 2, 1, 0 at planes 21, 13, 5; its copy-out runs at 3
-// again.  The decoder drops to 2 and 1 at planes 21 and 11 and to 0 only after
-// its plane loop, so a wave in the inverse transform (a quarter of a decode
-// wave's instructions) yields to every wave still decoding planes: with the
-// transform at the loop's last level the oldest wave of each SIMD finished
-// ~8 us before the youngest, which then ran alone.
+// again.  The decoder drops to 2 and 1 at planes 21 and 11, and a wave out of
+// its plane loop takes priority 2 again for the inverse transform and the
+// stores (CUZFP_DPRIO_AFTER).  Rounds 2-4 dropped it to 0 there, so that the
+// transform filled the plane-looping waves' gaps; but a SIMD's four decode
+// waves then ended at 13.2 / 15.4 / 18.0 / 20.6 us (profiles/r05_stamps.txt)
+// and the 64 MiB of output left only behind them.  Finishing a wave that is
+// out of the loop first starts its stores sooner: 256^3 r8 step 48.2-48.6 ->
+// 47.2-47.4 us on the polynomial field, 44.8-44.9 -> 44.6 on splitmix (2 at
+// 21/11; 3 measured 47.2-47.5 / 44.7-44.9, 3 with drops at 13/5 47.0-47.2 /
+// 44.9-45.0; 2D, 1D and f64 unchanged: profiles/r05_prio.txt).
 #ifndef CUZFP_PRIO_T2  // plane numbers (odd: the loops step by two) where the priority drops
 #define CUZFP_PRIO_T2 21
 #define CUZFP_PRIO_T1 13
@@ -687,7 +687,7 @@ ZFP_HD bool any_lane(bool p) {
 #define CUZFP_DPRIO_T2 21
 #define CUZFP_DPRIO_T1 11
 #define CUZFP_DPRIO_T0 (-1)
-#define CUZFP_DPRIO_AFTER 0
+#define CUZFP_DPRIO_AFTER 2
 #endif
 // The schedule pays off when the launch is one resident round of waves (256^3
 // f32: 4 waves per SIMD, all resident at once).  Over several rounds it costs
@@ -890,11 +890,9 @@ ZFP_HD void encode_plane_one_put(PW x, unsigned nf, uint64_t r, const PlaneLen& 
   // each before its first use: two s_waitcnt a plane)
   const uint32_t e0 = wr.sp0(byte_off4<0>(rl));
   const uint32_t e1 = N > 4 ? wr.sp1(byte_off4<1>(rl)) : 0u;
-#if !defined(CUZFP_EXP_EWAIT_OLD)  // (A/B builds: the compiler's two waits)
   sched_fence();
   wr.lds_wait();
   sched_fence();
-#endif
   uint32_t G = e0 >> 5;
   if constexpr (N > 4) G |= e1 << (e0 & 31u);
   const uint32_t g = low_bits(G, width);
@@ -1733,16 +1731,6 @@ ZFP_HD PW decode_plane_fast_any(unsigned& n, Reader& rd) {
   const unsigned nf = n;  // <= N-1
   // the group window first (the lookups wait on it), the verbatim window's
   // reads after the lookups' (Reader::window_g / window_w)
-#if defined(CUZFP_EXP_DWAIT_OLD)  // A/B builds: the compiler's waits
-  uint64_t w;
-  uint32_t g;
-  rd.windows(nf, w, g);
-  uint32_t e1, e2, e2a = 0, e2b = 0;
-  if constexpr (DIMS == 1)
-    e1 = rd.chunk1_fast(g);
-  else
-    rd.chunks_fast(g, e1, e2a, e2b);
-#else
   WRaw wr;
   const uint32_t g = rd.window_g(nf, wr);
   uint32_t e1, e2, e2a = 0, e2b = 0;
@@ -1754,7 +1742,6 @@ ZFP_HD PW decode_plane_fast_any(unsigned& n, Reader& rd) {
   rd.lds_wait();  // one wait for the lookups (and the window's dwords)
   sched_fence();
   const uint64_t w = rd.window_w_make(wr);
-#endif
   if constexpr (DIMS == 1) {
     e2 = 0;
   } else {
@@ -2234,9 +2221,6 @@ ZFP_HD bool decode_block(Scalar* f, unsigned maxbits, Reader& rd) {
     // decode.c:352-381
     const uint64_t head = rd.peek();
     const bool coded = head & 1;
-#if defined(CUZFP_EXP_ZB_LANE)  // A/B builds: round 4's per-lane return of a zero block
-    if (!coded) return false;
-#endif
     // A zero block (decode.c:354-355) takes the coded path with no budget
     // inside a wave that holds coded blocks: it reads no planes, so its q
     // are zero and its values 0 * 2^(emax-p+2) = +0 whatever its header bits

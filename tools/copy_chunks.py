@@ -83,6 +83,22 @@ def main():
                  "waited_GBps": round(nbytes / t2 / 1e9, 2)}
             res[f"{name}_{k}"] = r
             print(name, json.dumps(r), flush=True)
+    # the same chunks alternating between two streams (two copy engines), so
+    # that one copy's own cost overlaps the other's transfer
+    def copies2(k, kind):
+        c = nbytes // k
+        for i in range(k):
+            off = i * c
+            s = st[i % 2]
+            if kind == H2D:
+                ok(hip.hipMemcpyAsync(vp(d.value + off), vp(h.value + off), sz(c), H2D, s))
+            else:
+                ok(hip.hipMemcpyAsync(vp(h2.value + off), vp(d.value + off), sz(c), D2H, s))
+    for kind, name in ((H2D, "h2d"), (D2H, "d2h")):
+        for k in (4, 8, 16):
+            t = timed(lambda: copies2(k, kind))
+            res[f"{name}_{k}_two_streams_GBps"] = round(nbytes / t / 1e9, 2)
+            print(name, k, "chunks on two streams", res[f"{name}_{k}_two_streams_GBps"], flush=True)
     # full duplex: H2D on stream 0 beside D2H on stream 2, the whole buffer each
     t = timed(lambda: (copies(1, H2D, st[0]), copies(1, D2H, st[2], src=d2)))
     res["duplex_each_GBps"] = round(nbytes / t / 1e9, 2)
