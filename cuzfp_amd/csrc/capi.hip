@@ -157,6 +157,13 @@ static char* mapped_view(const void* p, size_t bytes) {
   return ok ? (char*)d : nullptr;
 }
 
+// CUZFP_HOST_SPLIT=0: fill the ordered schedule's queues chunk by chunk
+// between pinned buffers too (A/B of host_pipeline's three passes)
+static bool host_split_passes() {
+  const char* e = getenv("CUZFP_HOST_SPLIT");
+  return !(e && *e == '0');
+}
+
 static bool is_pinned_host(const void* ptr) {
   hipPointerAttribute_t a;
   const hipError_t e = hipPointerGetAttributes(&a, ptr);
@@ -248,6 +255,23 @@ struct PipelineCache {
   hipEvent_t ev_in[kMaxStreams] = {}, ev_kernel[kMaxStreams] = {}, ev_done[kMaxStreams] = {};
   HostBuf pin_in[kMaxStreams], pin_out[kMaxStreams];
   int nst = 0;
+  // one input-copy and one kernel event per chunk (the ordered schedule
+  // between pinned buffers enqueues every chunk's input copy first)
+  std::vector<hipEvent_t> ev_chunk_in, ev_chunk_kernel;
+  hipError_t chunk_events(size_t n) {
+    while (ev_chunk_in.size() < n) {
+      hipEvent_t a = nullptr, b = nullptr;
+      hipError_t e = hipEventCreateWithFlags(&a, hipEventDisableTiming);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&b, hipEventDisableTiming);
+      if (e != hipSuccess) {
+        if (a) (void)hipEventDestroy(a);
+        return e;
+      }
+      ev_chunk_in.push_back(a);
+      ev_chunk_kernel.push_back(b);
+    }
+    return hipSuccess;
+  }
 };
 
 // by device ordinal; kept for the process lifetime unless released
@@ -428,6 +452,45 @@ static int host_pipeline(const Problem& p, bool encode, void* h_data, void* h_st
     // (i % S) only matter for the pinned staging buffers: a slot is reused
     // once its previous chunk's copies are done.
     hipStream_t sin = r.st[0], sk = r.st[1], sout = r.st[2];
+    if (in_pinned && (out_pinned || out_view) && host_split_passes()) {
+      // Between pinned buffers nothing waits on the host, so the queues are
+      // filled in three passes -- every input copy, then every kernel, then
+      // every output copy -- each chunk's input and kernel with an event of
+      // its own.  (Filled chunk by chunk, an input copy was submitted after
+      // the previous chunk's output copy, which waits on that chunk's kernel,
+      // and the trace showed the input copies of a decompression starting
+      // only after that kernel, 12-48 us late: tools/host_trace.py,
+      // profiles/r05_host_trace_chunkwise.txt; in three passes
+      // r05_host_trace.txt.  Decompression 48.7 -> 50.1 GB/s, compression
+      // 49.2 -> 49.5: profiles/r05_host_sweep.txt.)
+      CUZFP_HIP_TRY(r.chunk_events(n));
+      for (size_t i = 0; i < n; i++) {
+        const Chunk& c = chunks[i];
+        const size_t i0 = encode ? c.d0 : c.s0, i1 = encode ? c.d1 : c.s1;
+        if (i1 > i0)
+          CUZFP_HIP_TRY(hipMemcpyAsync((encode ? dd : ds) + i0, (encode ? hd : hs) + i0, i1 - i0,
+                                       hipMemcpyHostToDevice, sin));
+        CUZFP_HIP_TRY(hipEventRecord(r.ev_chunk_in[i], sin));
+      }
+      for (size_t i = 0; i < n; i++) {
+        const Chunk& c = chunks[i];
+        CUZFP_HIP_TRY(hipStreamWaitEvent(sk, r.ev_chunk_in[i], 0));
+        int rc = encode ? launch_encode(p, dd, (uint64_t*)ds, c.w0, c.w1 - c.w0, sk)
+                        : launch_decode(p, (const uint64_t*)ds, out_view ? out_view : dd, c.w0, c.w1 - c.w0, sk);
+        if (rc) return rc;
+        CUZFP_HIP_TRY(hipEventRecord(r.ev_chunk_kernel[i], sk));
+      }
+      if (out_view) return CUZFP_SUCCESS;  // the kernels stored to the pinned array themselves
+      for (size_t i = 0; i < n; i++) {
+        size_t o0, o1;
+        out_range(chunks[i], &o0, &o1);
+        CUZFP_HIP_TRY(hipStreamWaitEvent(sout, r.ev_chunk_kernel[i], 0));
+        if (o1 > o0)
+          CUZFP_HIP_TRY(hipMemcpyAsync((encode ? hs : hd) + o0, (encode ? ds : dd) + o0, o1 - o0,
+                                       hipMemcpyDeviceToHost, sout));
+      }
+      return CUZFP_SUCCESS;
+    }
     for (size_t i = 0; i < n + S; i++) {
       if (i >= (size_t)S) {
         const size_t j = i - S;
@@ -670,6 +733,12 @@ int cuzfp_hip_release_host_cache(int device) {
     (void)hipEventDestroy(r.ev_done[i]);
     (void)hipStreamDestroy(r.st[i]);
   }
+  for (size_t i = 0; i < r.ev_chunk_in.size(); i++) {
+    (void)hipEventDestroy(r.ev_chunk_in[i]);
+    (void)hipEventDestroy(r.ev_chunk_kernel[i]);
+  }
+  r.ev_chunk_in.clear();
+  r.ev_chunk_kernel.clear();
   r.nst = 0;
   CUZFP_HIP_TRY(hipSetDevice(prev));
   return CUZFP_SUCCESS;

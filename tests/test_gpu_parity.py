@@ -526,9 +526,11 @@ def test_host_pipeline_multi_chunk(cuda, restatement, monkeypatch, shape, dtype,
     if pinned:
         a = torch.from_numpy(a).pin_memory().numpy()
         out = torch.empty(cz.stream_bytes(shape, dtype, mb) // 8, dtype=torch.int64).pin_memory().numpy().view(np.uint64)
+    yout = torch.empty(shape, dtype=torch.from_numpy(a).dtype).pin_memory().numpy() if pinned else None
     slab = a.nbytes // (shape[0] // 4 if len(shape) > 1 else max(1, shape[0] // 4))
     # 8 slabs a chunk and a.nbytes // 7 (1D, 2D) run the ordered schedule's
-    # halving edge chunks (capi.hip host_pipeline)
+    # growing edge chunks (capi.hip host_pipeline); pinned buffers both ways
+    # its three-pass queue filling
     for chunk in (1, 3 * slab + 5, 8 * slab, a.nbytes // 7):
         monkeypatch.setenv("CUZFP_HOST_CHUNK_BYTES", str(chunk))
         for nstreams in (1, 2, 3):
@@ -536,6 +538,10 @@ def test_host_pipeline_multi_chunk(cuda, restatement, monkeypatch, shape, dtype,
             assert np.array_equal(s, ref), (chunk, nstreams)
             y = cz.decompress_host(s, shape, dtype, mb, nstreams=nstreams)
             assert np.array_equal(y, want), (chunk, nstreams)
+            if pinned:
+                yout.fill(7)
+                y = cz.decompress_host(s, shape, dtype, mb, nstreams=nstreams, out=yout)
+                assert np.array_equal(y, want), (chunk, nstreams, "pinned out")
 
 
 def test_broadcast_view_encodes_materialised(cuda, restatement):

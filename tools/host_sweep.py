@@ -56,9 +56,11 @@ def main():
     s_np = h_s.numpy().view(np.uint64)
     d.copy_(h_in)
     want = cz.decode(cz.encode(d, mb), arr.shape, d.dtype, mb).cpu().numpy().view(np.uint32)
-    for zc, ordered, chunks in (("0", "0", (8,)), ("0", "1", (16, 32, 64)), ("1", "1", (32,))):
+    for zc, ordered, split, chunks in (("0", "0", "1", (8,)), ("0", "1", "0", (32, 64)), ("0", "1", "1", (16, 32, 64)),
+                                       ("1", "1", "1", (64,)), ("2", "1", "1", (64,))):
         os.environ["CUZFP_HOST_ZEROCOPY"] = zc
         os.environ["CUZFP_HOST_ORDERED"] = ordered
+        os.environ["CUZFP_HOST_SPLIT"] = split
         for chunk_mb in chunks:
             os.environ["CUZFP_HOST_CHUNK_BYTES"] = str(chunk_mb << 20)
             ns = 4
@@ -66,7 +68,7 @@ def main():
             dcp = rate(lambda: cz.decompress_host(s_np, arr.shape, np.float32, mb, nstreams=ns, out=h_out.numpy()),
                        arr.nbytes)
             ok = bool(np.array_equal(h_out.numpy().view(np.uint32), want))
-            r = {"zero_copy": zc, "ordered": ordered, "chunk_MiB": chunk_mb, "nstreams": ns, "compress_GBps": c,
+            r = {"zero_copy": zc, "ordered": ordered, "split": split, "chunk_MiB": chunk_mb, "nstreams": ns, "compress_GBps": c,
                  "decompress_GBps": dcp, "roundtrip_equal": ok}
             res["runs"].append(r)
             print(json.dumps(r), flush=True)

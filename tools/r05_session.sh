@@ -37,6 +37,12 @@ for s in "$@"; do
     ranges)
       timeout -k 10 120 python tools/zero_copy.py --ranges > "$OUT/ranges_${TAG}.txt" 2>&1
       stop_on $? ranges; cat "$OUT/ranges_${TAG}.txt" ;;
+    hosttrace)
+      rm -rf "$OUT/htrace_${TAG}"
+      timeout -k 10 180 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$OUT/htrace_${TAG}" -o run -- \
+        python tools/host_trace.py > "$OUT/htrace_${TAG}.log" 2>&1
+      stop_on $? hosttrace
+      python tools/host_trace.py --analyse "$OUT/htrace_${TAG}" > "$OUT/htrace_${TAG}.txt" 2>&1; head -80 "$OUT/htrace_${TAG}.txt" ;;
     zerocopy)
       timeout -k 10 300 python tools/zero_copy.py > "$OUT/zero_copy_${TAG}.txt" 2>&1
       stop_on $? zerocopy; cat "$OUT/zero_copy_${TAG}.txt" ;;
