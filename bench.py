@@ -722,16 +722,17 @@ def main():
             hp_back = torch.empty(a.shape, dtype=x.dtype).pin_memory().numpy()
             cz.compress_host(hp_in, maxbits, out=hp_out)
             cz.decompress_host(hp_out, shape, dtype, maxbits, out=hp_back)
-            tc = time.perf_counter()
-            for _ in range(5):
-                cz.compress_host(hp_in, maxbits, out=hp_out)
-            tc = (time.perf_counter() - tc) / 5
-            td = time.perf_counter()
-            for _ in range(5):
-                cz.decompress_host(hp_out, shape, dtype, maxbits, out=hp_back)
-            td = (time.perf_counter() - td) / 5
+            def med7(fn):  # median of 7 synchronous calls
+                ts = []
+                for _ in range(7):
+                    t0 = time.perf_counter()
+                    fn()
+                    ts.append(time.perf_counter() - t0)
+                return sorted(ts)[3]
+            tc = med7(lambda: cz.compress_host(hp_in, maxbits, out=hp_out))
+            td = med7(lambda: cz.decompress_host(hp_out, shape, dtype, maxbits, out=hp_back))
             # the bare pinned link in the same run: one copy of the array each
-            # way (the larger of each call's two transfers), 5 each
+            # way (the larger of each call's two transfers), mean of 5 each
             h_in = torch.from_numpy(hp_in)
             h_back = torch.from_numpy(hp_back)
             d_tmp = torch.empty(a.shape, dtype=x.dtype, device=dev)
@@ -763,7 +764,7 @@ def main():
                          "chunk_bytes": int(os.environ.get("CUZFP_HOST_CHUNK_BYTES", 64 << 20)), "nstreams": 4,
                          "schedule": "per-stream" if os.environ.get("CUZFP_HOST_ORDERED", "1") == "0" else "ordered",
                          "zero_copy": int(os.environ.get("CUZFP_HOST_ZEROCOPY", "0") or 0),
-                         "note": "pinned host buffers, PCIe-inclusive (cuzfp_hip_compress_host/decompress_host); "
+                         "note": "pinned host buffers, PCIe-inclusive (cuzfp_hip_compress_host/decompress_host), median of 7 calls; "
                                  "frac_of_link = rate over the larger transfer's one-way link rate: compress "
                                  "array bytes / max(array/h2d, stream/d2h), decompress array bytes / "
                                  "max(array/d2h, stream/h2d); H2D beside D2H run at ~48 GB/s each "
