@@ -46,6 +46,9 @@ for s in "$@"; do
     zerocopy)
       timeout -k 10 300 python tools/zero_copy.py > "$OUT/zero_copy_${TAG}.txt" 2>&1
       stop_on $? zerocopy; cat "$OUT/zero_copy_${TAG}.txt" ;;
+    stamps64)
+      timeout -k 10 300 python tools/probe.py stamps --lib p9 --dtype float64 --rate 16 --back 2 > "$OUT/stamps64_${TAG}.txt" 2>&1
+      stop_on $? stamps64; cat "$OUT/stamps64_${TAG}.txt" ;;
     launch)
       timeout -k 10 300 python tools/launch_overhead.py > "$OUT/launch_${TAG}.txt" 2>&1
       stop_on $? launch; cat "$OUT/launch_${TAG}.txt" ;;
