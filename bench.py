@@ -763,7 +763,7 @@ def main():
                                           "decompress": round(n_in / td / 1e9 / d_link, 3)},
                          "chunk_bytes": int(os.environ.get("CUZFP_HOST_CHUNK_BYTES", 64 << 20)), "nstreams": 4,
                          "schedule": "per-stream" if os.environ.get("CUZFP_HOST_ORDERED", "1") == "0" else "ordered",
-                         "zero_copy": int(os.environ.get("CUZFP_HOST_ZEROCOPY", "0") or 0),
+                         "zero_copy": int(os.environ.get("CUZFP_HOST_ZEROCOPY", "1") or 0),
                          "note": "pinned host buffers, PCIe-inclusive (cuzfp_hip_compress_host/decompress_host), median of 7 calls; "
                                  "frac_of_link = rate over the larger transfer's one-way link rate: compress "
                                  "array bytes / max(array/h2d, stream/d2h), decompress array bytes / "

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cstring>
 #include <mutex>
+#include <chrono>
 #include <vector>
 
 #include "launch.hpp"
@@ -85,6 +86,24 @@ static size_t stream_bytes_of(const Geometry& g) {
 static uint32_t waves_of(const Geometry& g) { return (g.nblocks + kLanes - 1) / kLanes; }
 
 
+// Bandwidth calibrator (cuzfp_hip_copy, below; also the stand-in kernel of
+// pick_copy_queues): a device-to-device copy with 16-byte
+// non-temporal loads and stores, one per lane, one grid over the whole buffer
+// -- the codec's own access width, cache policy and one-touch-per-wave shape.
+// bench.py times it at 1 GiB beside the codec as the achievable-HBM reference
+// (roofline.frac_of_copy).  tools/ubench/copy.hip (profiles/r02_copy_ubench.txt):
+// this shape 6.64 TB/s (read + write) at 1 GiB; grid-stride loops over
+// 1-32 workgroups per CU with 1-8 accesses in flight a lane 4.6-6.4 TB/s;
+// plain (temporal) accesses 0.3-0.5 TB/s below non-temporal.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void copy16_nt(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                 size_t n16) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride)
+    __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+}
+
 // ---------------------------------------------------------------------------
 // Host-memory pipeline (cuzfp_hip_compress_host / cuzfp_hip_decompress_host).
 //
@@ -126,18 +145,21 @@ static bool host_ordered() {
   return !(e && *e == '0');
 }
 
-// Zero-copy level (CUZFP_HOST_ZEROCOPY, opt-in): 0 (default) none; 1:
-// compression of a pinned array into a pinned stream is one encode launch that
-// loads the array and stores the stream over PCIe itself; 2: also
-// decompression into a pinned array, the decode kernels storing to it (the
-// stream still copied in chunks).  256^3 f32 rate 8 (tools/zero_copy.py,
-// tools/host_sweep.py, profiles/r05_host_sweep.txt): compression 50.2 GB/s
-// against 50.4 for the copy pipeline, decompression 42.3 against 48.9 -- the
-// kernels' own PCIe stores reach 49.6 GB/s (53.1 for a plain copy kernel)
-// where the copy engine reaches 55.
+// Zero-copy level (CUZFP_HOST_ZEROCOPY): 0 none; 1 (default): compression of
+// a pinned array into a pinned stream is one encode launch that loads the
+// array and stores the stream over PCIe itself; 2: also decompression into a
+// pinned array, the decode kernels storing to it (the stream still copied in
+// chunks).  256^3 f32 rate 8 (tools/zero_copy.py,
+// tools/host_sweep.py, tools/hostpath_probe.py, profiles/r05_host_*.txt):
+// compression 50.2-50.6 GB/s whatever streams the process made before, where
+// the copy pipeline measured 47-51 after its queue calibration
+// (pick_copy_queues) and 41 without it; decompression at level 2 42-43
+// (with the kernels also loading the stream: 41-42) against 49-50 for the copies -- the kernels' own PCIe stores
+// reach 49.6 GB/s (53.1 for a plain copy kernel) where the copy engine
+// reaches 55-57.  So compression uses level 1 and decompression the copies.
 static int host_zero_copy() {
   const char* e = getenv("CUZFP_HOST_ZEROCOPY");
-  return (e && *e) ? atoi(e) : 0;
+  return (e && *e) ? atoi(e) : 1;
 }
 
 // The device address of [p, p + bytes) when the whole range lies in one pinned
@@ -255,6 +277,9 @@ struct PipelineCache {
   hipEvent_t ev_in[kMaxStreams] = {}, ev_kernel[kMaxStreams] = {}, ev_done[kMaxStreams] = {};
   HostBuf pin_in[kMaxStreams], pin_out[kMaxStreams];
   int nst = 0;
+  // the ordered schedule's queues: indices into st (pick_copy_queues)
+  int q_in = 0, q_k = 1, q_out = 2;
+  bool queues_picked = false;
   // one input-copy and one kernel event per chunk (the ordered schedule
   // between pinned buffers enqueues every chunk's input copy first)
   std::vector<hipEvent_t> ev_chunk_in, ev_chunk_kernel;
@@ -304,6 +329,104 @@ struct CallBuf {
       return CUZFP_ERROR_HIP;       \
     }                               \
   } while (0)
+
+// Which of the cache's first eight streams carry the input copies, the
+// kernels and the output copies.  HIP spreads streams over GPU_MAX_HW_QUEUES
+// (4 on these boxes) hardware queues in creation order, and the same pipeline
+// ran at 50 GB/s each way or at 41 according to how many streams the process
+// had created before it (tools/hostpath_probe.py --streams N,
+// profiles/r05_hostpath_streams.txt: N = 0, 1, 4, 5 fast, 2, 3 slow).  Among
+// four consecutive streams no assignment was fast for N = 2; among eight one
+// was (profiles/r05_host_queues.txt).  So, once per device, a small model of
+// the schedule -- three 4 MiB chunks, each an H2D copy, a copy kernel waiting
+// on it and a D2H copy waiting on the kernel -- is timed for each choice of
+// one role's stream with the other two held (output, then kernels, then
+// input; 16 candidates, the better of two ~0.4 ms runs each) and the
+// fastest assignment is kept.
+#ifndef CUZFP_PICK_STREAMS
+#define CUZFP_PICK_STREAMS 8
+#endif
+constexpr int kPickStreams = CUZFP_PICK_STREAMS;
+static hipError_t pick_copy_queues(PipelineCache& r) {
+  constexpr size_t kB = 4u << 20;
+  constexpr int kChunks = 3;
+  void *h = nullptr, *d = nullptr;
+  hipError_t e = hipHostMalloc(&h, 2 * kChunks * kB, hipHostMallocDefault);
+  if (e == hipSuccess) e = hipMalloc(&d, 2 * kChunks * kB);
+  if (e != hipSuccess) {
+    if (h) (void)hipHostFree(h);
+    return e;
+  }
+  std::memset(h, 0, 2 * kChunks * kB);
+  char* hc = (char*)h;
+  char* dc = (char*)d;
+  hipEvent_t ev[2 * kChunks] = {};
+  for (int i = 0; i < 2 * kChunks && e == hipSuccess; i++) e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
+  const unsigned grid = (unsigned)(kB / 16 / 256);
+  // every stream copies both ways once before anything is timed
+  for (int q = 0; q < kPickStreams && e == hipSuccess; q++) {
+    e = hipMemcpyAsync(dc, hc, kB, hipMemcpyHostToDevice, r.st[q]);
+    if (e == hipSuccess) e = hipMemcpyAsync(hc + kB, dc + kB, kB, hipMemcpyDeviceToHost, r.st[q]);
+    if (e == hipSuccess) e = hipStreamSynchronize(r.st[q]);
+  }
+  auto trial1 = [&](int a, int k, int b, double& t) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int c = 0; c < kChunks && e == hipSuccess; c++) {
+      e = hipMemcpyAsync(dc + c * kB, hc + c * kB, kB, hipMemcpyHostToDevice, r.st[a]);
+      if (e == hipSuccess) e = hipEventRecord(ev[c], r.st[a]);
+    }
+    for (int c = 0; c < kChunks && e == hipSuccess; c++) {
+      e = hipStreamWaitEvent(r.st[k], ev[c], 0);
+      if (e == hipSuccess) {
+        hipLaunchKernelGGL(copy16_nt, dim3(grid), dim3(256), 0, r.st[k], (const u32x4*)(dc + c * kB),
+                           (u32x4*)(dc + (kChunks + c) * kB), kB / 16);
+        e = hipGetLastError();
+      }
+      if (e == hipSuccess) e = hipEventRecord(ev[kChunks + c], r.st[k]);
+    }
+    for (int c = 0; c < kChunks && e == hipSuccess; c++) {
+      e = hipStreamWaitEvent(r.st[b], ev[kChunks + c], 0);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(hc + (kChunks + c) * kB, dc + (kChunks + c) * kB, kB, hipMemcpyDeviceToHost, r.st[b]);
+    }
+    for (int q : {a, k, b})
+      if (e == hipSuccess) e = hipStreamSynchronize(r.st[q]);
+    t = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (getenv("CUZFP_HOST_DEBUG")) fprintf(stderr, "cuzfp host queues: in %d kernels %d out %d: %.1f us\n", a, k, b, t * 1e6);
+  };
+  auto trial = [&](int a, int k, int b, double& t) {  // the better of two runs
+    double t2 = 0;
+    trial1(a, k, b, t);
+    trial1(a, k, b, t2);
+    t = std::min(t, t2);
+  };
+  int role[3] = {0, 1, 2};  // in, kernels, out
+  double best = 1e30;
+  trial(role[0], role[1], role[2], best);
+  for (int which : {2, 1, 0}) {
+    for (int q = 0; q < kPickStreams && e == hipSuccess; q++) {
+      if (q == role[0] || q == role[1] || q == role[2]) continue;
+      int cand[3] = {role[0], role[1], role[2]};
+      cand[which] = q;
+      double t = 0;
+      trial(cand[0], cand[1], cand[2], t);
+      if (t < best) {
+        best = t;
+        role[which] = q;
+      }
+    }
+  }
+  for (int i = 0; i < 2 * kChunks; i++)
+    if (ev[i]) (void)hipEventDestroy(ev[i]);
+  (void)hipFree(d);
+  (void)hipHostFree(h);
+  if (e != hipSuccess) return e;
+  r.q_in = role[0];
+  r.q_k = role[1];
+  r.q_out = role[2];
+  r.queues_picked = true;
+  return hipSuccess;
+}
 
 static int host_pipeline(const Problem& p, bool encode, void* h_data, void* h_stream,
                          int nstreams) {
@@ -406,8 +529,8 @@ static int host_pipeline(const Problem& p, bool encode, void* h_data, void* h_st
   }
   const bool in_pinned = encode ? data_pinned : stream_pinned;
   const bool out_pinned = encode ? stream_pinned : data_pinned;
-  // the ordered schedule uses three streams whatever S is
-  const int NS = ordered ? std::max(S, 3) : S;
+  // the ordered schedule uses three of four streams whatever S is
+  const int NS = ordered ? std::max(S, kPickStreams) : S;
   for (int i = r.nst; i < NS; i++) {
     CUZFP_HIP_TRY(hipStreamCreateWithFlags(&r.st[i], hipStreamNonBlocking));
     CUZFP_HIP_TRY(hipEventCreateWithFlags(&r.ev_in[i], hipEventDisableTiming));
@@ -415,6 +538,7 @@ static int host_pipeline(const Problem& p, bool encode, void* h_data, void* h_st
     CUZFP_HIP_TRY(hipEventCreateWithFlags(&r.ev_done[i], hipEventDisableTiming));
     r.nst = i + 1;
   }
+  if (ordered && !r.queues_picked) CUZFP_HIP_TRY(pick_copy_queues(r));
   CallHostBuf pin_in[kMaxStreams], pin_out[kMaxStreams];
   for (int i = 0; i < S; i++) {
     if (!in_pinned) CUZFP_HIP_TRY(pin_in[i].get(r.pin_in[i], max_in));
@@ -451,7 +575,7 @@ static int host_pipeline(const Problem& p, bool encode, void* h_data, void* h_st
     // last chunk's kernel and output copy trail the input stream.  Slots
     // (i % S) only matter for the pinned staging buffers: a slot is reused
     // once its previous chunk's copies are done.
-    hipStream_t sin = r.st[0], sk = r.st[1], sout = r.st[2];
+    hipStream_t sin = r.st[r.q_in], sk = r.st[r.q_k], sout = r.st[r.q_out];
     if (in_pinned && (out_pinned || out_view) && host_split_passes()) {
       // Between pinned buffers nothing waits on the host, so the queues are
       // filled in three passes -- every input copy, then every kernel, then
@@ -588,24 +712,6 @@ static int host_pipeline(const Problem& p, bool encode, void* h_data, void* h_st
 }
 
 // ---------------------------------------------------------------------------
-// Bandwidth calibrator (cuzfp_hip_copy): a device-to-device copy with 16-byte
-// non-temporal loads and stores, one per lane, one grid over the whole buffer
-// -- the codec's own access width, cache policy and one-touch-per-wave shape.
-// bench.py times it at 1 GiB beside the codec as the achievable-HBM reference
-// (roofline.frac_of_copy).  tools/ubench/copy.hip (profiles/r02_copy_ubench.txt):
-// this shape 6.64 TB/s (read + write) at 1 GiB; grid-stride loops over
-// 1-32 workgroups per CU with 1-8 accesses in flight a lane 4.6-6.4 TB/s;
-// plain (temporal) accesses 0.3-0.5 TB/s below non-temporal.
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-__global__ __launch_bounds__(256) void copy16_nt(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
-                                                 size_t n16) {
-  const size_t stride = (size_t)gridDim.x * blockDim.x;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride)
-    __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
-}
-
 }  // namespace cuzfp
 
 
@@ -740,6 +846,7 @@ int cuzfp_hip_release_host_cache(int device) {
   r.ev_chunk_in.clear();
   r.ev_chunk_kernel.clear();
   r.nst = 0;
+  r.queues_picked = false;
   CUZFP_HIP_TRY(hipSetDevice(prev));
   return CUZFP_SUCCESS;
 }

@@ -120,8 +120,11 @@ int cuzfp_hip_decode(const uint64_t* d_stream, size_t stream_bytes, int type, un
  * Synchronous; contiguous arrays only.  Environment (read per call):
  * CUZFP_HOST_CHUNK_BYTES sets the chunk size, CUZFP_HOST_ORDERED=0 selects
  * round 4's schedule (chunk i's copies and kernel on stream i % nstreams),
- * CUZFP_HOST_ZEROCOPY=1/2 lets the kernels load / store pinned buffers
- * directly (opt-in; capi.hip host_zero_copy has the measurements).
+ * CUZFP_HOST_ZEROCOPY: 1 (default) compresses a pinned array into a pinned
+ * stream in one kernel that loads and stores them over PCIe itself, 2 also
+ * lets the decode kernels store to a pinned array, 0 copies everything
+ * (capi.hip host_zero_copy has the measurements).  The first call on a device
+ * also times which of its streams carry which copies (~15 ms, once).
  *
  * Retention: the first call on a device allocates, and keeps for later calls,
  * device buffers for the array and the stream (grown to the largest call, up

@@ -26,6 +26,15 @@ sys.path.insert(0, ROOT)
 def run():
     import torch
     import cuzfp_amd as cz
+    # --streams N: N torch streams used before the pipeline creates its own
+    nst = int(sys.argv[sys.argv.index("--streams") + 1]) if "--streams" in sys.argv else 0
+    keep = []
+    for _ in range(nst):
+        st = torch.cuda.Stream()
+        with torch.cuda.stream(st):
+            keep.append(torch.ones(16, device="cuda") * 2)
+        keep.append(st)
+    torch.cuda.synchronize()
     from cuzfp_amd.datagen import polynomial_field
     arr = polynomial_field((256,) * 3, np.float32)
     mb = cz.rate_to_maxbits(8, np.float32, 3)
