@@ -667,8 +667,11 @@ ZFP_HD bool any_lane(bool p) {
 // coder together instead of oldest-first (which leaves the last wave running
 // alone at the end, at a fraction of the SIMD's issue rate).
 //
-// The encoder drops to 2, 1, 0 at planes 21, 13, 5; its copy-out runs at 3
-// again.  The decoder drops to 2 and 1 at planes 21 and 11, and a wave out of
+// The encoder drops to 2, 1, 0 at planes 17, 9, 1; its copy-out runs at 3
+// again.  (Rounds 1-4: 21, 13, 5.  Round 5, after the decoder change below,
+// four interleaved A/B rounds: 256^3 r8 step 47.2-47.7 -> 46.6-46.8 us on
+// the polynomial field, the headline's, and 44.5-44.9 -> 44.7-45.0 on
+// splitmix; 19/11/3 in between, profiles/r05_xvar_encoder_prio.txt.)  The decoder drops to 2 and 1 at planes 21 and 11, and a wave out of
 // its plane loop takes priority 2 again for the inverse transform and the
 // stores (CUZFP_DPRIO_AFTER).  Rounds 2-4 dropped it to 0 there, so that the
 // transform filled the plane-looping waves' gaps; but a SIMD's four decode
@@ -679,9 +682,9 @@ ZFP_HD bool any_lane(bool p) {
 // 21/11; 3 measured 47.2-47.5 / 44.7-44.9, 3 with drops at 13/5 47.0-47.2 /
 // 44.9-45.0; 2D, 1D and f64 unchanged: profiles/r05_prio.txt).
 #ifndef CUZFP_PRIO_T2  // plane numbers (odd: the loops step by two) where the priority drops
-#define CUZFP_PRIO_T2 21
-#define CUZFP_PRIO_T1 13
-#define CUZFP_PRIO_T0 5
+#define CUZFP_PRIO_T2 17
+#define CUZFP_PRIO_T1 9
+#define CUZFP_PRIO_T0 1
 #endif
 #ifndef CUZFP_DPRIO_T2
 #define CUZFP_DPRIO_T2 21
