@@ -450,9 +450,9 @@ static int host_pipeline(const Problem& p, bool encode, void* h_data, void* h_st
   // pipeline's exposed end -- the last chunks of a compression, whose kernels
   // and stream copies trail the input copies, and the first of a
   // decompression, before whose kernel no output copy can start -- which grow
-  // by 3x from about nslabs / 32 (256^3 f32, 1 MiB slabs, at 32 MiB chunks:
-  // compression 19, 19, 18, 6, 2 slabs; decompression 2, 6, 18, 19, 19).  The stream is a
-  // quarter of the data or less, so chunk i + 1's stream copy and kernel
+  // by 3x from about nslabs / 32 (256^3 f32, 1 MiB slabs, 64 MiB chunks:
+  // compression 38, 18, 6, 2 slabs; decompression 2, 6, 18, 38).  The stream
+  // is a quarter of the data or less, so chunk i + 1's stream copy and kernel
   // finish within chunk i's data copy at 3x growth, and the copy queue that
   // binds never waits; every copy also costs ~10-15 us of its own
   // (tools/copy_chunks.py), so the chunks stay few.
@@ -529,7 +529,8 @@ static int host_pipeline(const Problem& p, bool encode, void* h_data, void* h_st
   }
   const bool in_pinned = encode ? data_pinned : stream_pinned;
   const bool out_pinned = encode ? stream_pinned : data_pinned;
-  // the ordered schedule uses three of four streams whatever S is
+  // the ordered schedule uses three of kPickStreams streams (pick_copy_queues)
+  // whatever S is
   const int NS = ordered ? std::max(S, kPickStreams) : S;
   for (int i = r.nst; i < NS; i++) {
     CUZFP_HIP_TRY(hipStreamCreateWithFlags(&r.st[i], hipStreamNonBlocking));
@@ -569,8 +570,8 @@ static int host_pipeline(const Problem& p, bool encode, void* h_data, void* h_st
     return launch_encode(p, in_view, (uint64_t*)out_view, 0, nwaves, r.st[0]);  // Drain waits for it
   }
   if (ordered) {
-    // three queues, each in chunk order: input copies on st[0], kernels on
-    // st[1], output copies on st[2].  Chunk i's input lands at (i + 1) input
+    // three queues, each in chunk order: input copies, kernels, output copies
+    // (on the streams pick_copy_queues chose).  Chunk i's input lands at (i + 1) input
     // copies' time, so its kernel and output copy start then, and only the
     // last chunk's kernel and output copy trail the input stream.  Slots
     // (i % S) only matter for the pinned staging buffers: a slot is reused
