@@ -73,6 +73,21 @@ def summary(ops: list) -> str:
             f"      top: {top}")
 
 
+def vgpr_counts(co: str) -> dict:
+    """kernel name -> .vgpr_count from the code object's metadata notes"""
+    notes = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", co],
+                           capture_output=True, text=True, check=True).stdout
+    out, vg = {}, None
+    for line in notes.splitlines():
+        m = re.match(r"\s+\.vgpr_count:\s+(\d+)", line)
+        if m:
+            vg = int(m.group(1))
+        m = re.match(r"\s+\.name:\s+(_Z\S+)", line)
+        if m:
+            out[m.group(1)] = vg
+    return out
+
+
 def first(ops, pred, start=0):
     for i in range(start, len(ops)):
         if pred(ops[i]):
@@ -83,14 +98,17 @@ def first(ops, pred, start=0):
 def main():
     obj = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "build", "obj", "inst_f32.o")
     ks = kernels(disassemble(obj))
+    meta = vgpr_counts(os.path.join(ROOT, "build", "isa", "f32.co"))
     for name, ops in ks.items():
         enc = re.search(r"zfp_encodeI[fd]Li3ELb1ELb1ELb(\d)", name)
-        dec = re.search(r"zfp_decodeI[fd]Li3ELb1ELb(\d)ELb0", name)
+        # zfp_decode<Scalar, 3, FAST=true, PRIO, ...>
+        dec = re.search(r"zfp_decodeI[fd]Li3ELb1ELb(\d)E", name)
         if not (enc or dec):
             continue
         kind = "encode" if enc else "decode"
         prio = (enc or dec).group(1) == "1"
-        print(f"== zfp_{kind}<float,3,FAST{',ALIGNED' if enc else ''},PRIO={int(prio)}>: {len(ops)} instructions")
+        print(f"== zfp_{kind}<float,3,FAST{',ALIGNED' if enc else ''},PRIO={int(prio)}>: {len(ops)} instructions, "
+              f"{meta.get(name, '?')} VGPRs")
         print("   whole  " + summary(ops))
         if enc:
             t0 = first(ops, lambda o: o == "v_perm_b32")
