@@ -41,16 +41,18 @@ def main():
             cz.encode(x, mb, out=w[0])
             cz.decode(w[0], shape, x.dtype, mb, out=y)
 
-    def pipelined():
+    def pipelined_on(sA, sB):
         # E_k on A; D_k on B after E_k; E_{k+2} (same buffer) after D_k
-        sA = torch.cuda.current_stream()  # the capture stream under a graph
-        sB.wait_stream(sA)
+        cur = torch.cuda.current_stream()
+        sA.wait_stream(cur)
+        sB.wait_stream(cur)
         done = [None, None]
         for k in range(K):
             b = k & 1
             if done[b] is not None:
                 sA.wait_event(done[b])
-            cz.encode(x, mb, out=w[b])
+            with torch.cuda.stream(sA):
+                cz.encode(x, mb, out=w[b])
             ev = torch.cuda.Event()
             ev.record(sA)
             sB.wait_event(ev)
@@ -59,7 +61,17 @@ def main():
             d = torch.cuda.Event()
             d.record(sB)
             done[b] = d
-        sA.wait_stream(sB)
+        cur.wait_stream(sA)
+        cur.wait_stream(sB)
+
+    def pipelined():  # the capture stream under a graph carries the encodes
+        pipelined_on(torch.cuda.current_stream(), sB)
+
+    # stream priorities (lower number = higher priority): the decodes' queue
+    # ahead of the encodes', so that decode k's workgroups are all dispatched
+    # before encode k+1's, which then take the slots decode k's waves free
+    lo, hi = torch.cuda.Stream(priority=0), torch.cuda.Stream(priority=-1)
+    lo2, hi2 = torch.cuda.Stream(priority=0), torch.cuda.Stream(priority=-1)
 
     def graphed(fn):
         g = torch.cuda.CUDAGraph()
@@ -67,7 +79,9 @@ def main():
             fn()
         return g.replay
 
-    variants = {"serial": graphed(serial), "pipe-eager": pipelined}
+    variants = {"serial": graphed(serial), "pipe-eager": pipelined,
+                "pipe-prio-dec": lambda: pipelined_on(lo, hi),
+                "pipe-prio-enc": lambda: pipelined_on(hi2, lo2)}
     try:
         variants["pipe-graph"] = graphed(pipelined)
     except Exception as e:  # pragma: no cover
@@ -89,7 +103,7 @@ def main():
         res[name] = round(sorted(r)[3], 2)
         print(f"{name:11s} {res[name]:8.2f} us per round trip", flush=True)
     # the pipelined round trips decode to the same array
-    pipelined()
+    pipelined_on(lo, hi)
     torch.cuda.synchronize()
     assert torch.equal(w[0], ref) and torch.equal(w[1], ref)
     assert torch.equal(y, cz.decode(ref, shape, x.dtype, mb))
