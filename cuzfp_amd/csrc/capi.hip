@@ -788,6 +788,20 @@ int cuzfp_hip_decode(const uint64_t* d_stream, size_t stream_bytes, int type, un
   return launch_decode(p, d_stream, d_data, 0, waves_of(p.g), stream);
 }
 
+int cuzfp_hip_decode_encode(const uint64_t* d_stream_in, size_t stream_bytes, void* d_data_out,
+                            const void* d_data_in, uint64_t* d_stream_out, size_t stream_capacity,
+                            int type, unsigned nx, unsigned ny, unsigned nz, unsigned maxbits,
+                            hipStream_t stream) {
+  Problem p;
+  int rc = make_problem(type, nx, ny, nz, 0, 0, 0, maxbits, &p);
+  if (rc) return rc;
+  if (!d_stream_in || !d_data_out || !d_data_in || !d_stream_out) return CUZFP_ERROR_INVALID_ARGUMENT;
+  const size_t need = stream_bytes_of(p.g);
+  if (stream_bytes < need || stream_capacity < need) return CUZFP_ERROR_BUFFER_TOO_SMALL;
+  if (type != CUZFP_TYPE_FLOAT) return CUZFP_ERROR_UNSUPPORTED_TYPE;
+  return launch_decode_encode_type<float>(p, d_stream_in, d_data_out, d_data_in, d_stream_out, stream);
+}
+
 int cuzfp_hip_copy(const void* d_src, void* d_dst, size_t bytes, hipStream_t stream) {
   if (!d_src || !d_dst || (bytes & 15) || (((uintptr_t)d_src | (uintptr_t)d_dst) & 15))
     return CUZFP_ERROR_INVALID_ARGUMENT;

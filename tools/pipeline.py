@@ -23,6 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--only", default="", help="comma-separated variant names")
     a = ap.parse_args()
     import torch
     import cuzfp_amd as cz
@@ -79,11 +80,21 @@ def main():
             fn()
         return g.replay
 
-    variants = {"serial": graphed(serial), "pipe-eager": pipelined,
+    def fused():
+        # E_0; then decode k and encode k+1 in one launch; D_{K-1}
+        cz.encode(x, mb, out=w[0])
+        for k in range(K - 1):
+            cz.decode_encode(w[k & 1], y, x, w[(k + 1) & 1], mb)
+        cz.decode(w[(K - 1) & 1], shape, x.dtype, mb, out=y)
+
+    variants = {"serial": graphed(serial), "fused": graphed(fused), "fused-eager": fused, "pipe-eager": pipelined,
                 "pipe-prio-dec": lambda: pipelined_on(lo, hi),
                 "pipe-prio-enc": lambda: pipelined_on(hi2, lo2)}
+    if a.only:
+        variants = {k: v for k, v in variants.items() if k in a.only.split(",")}
     try:
-        variants["pipe-graph"] = graphed(pipelined)
+        if not a.only or "pipe-graph" in a.only.split(","):
+            variants["pipe-graph"] = graphed(pipelined)
     except Exception as e:  # pragma: no cover
         print("pipe-graph capture failed:", e)
     res = {}
@@ -103,8 +114,16 @@ def main():
         res[name] = round(sorted(r)[3], 2)
         print(f"{name:11s} {res[name]:8.2f} us per round trip", flush=True)
     # the pipelined round trips decode to the same array
-    pipelined_on(lo, hi)
-    torch.cuda.synchronize()
+    for f in (pipelined_on, None):
+        w[0].zero_(); w[1].zero_(); y.zero_()
+        if f is None:
+            fused()
+        else:
+            f(lo, hi)
+        torch.cuda.synchronize()
+        assert torch.equal(w[0], ref) and torch.equal(w[1], ref)
+        assert torch.equal(y, cz.decode(ref, shape, x.dtype, mb))
+    print("pipelined and fused round trips: streams and decode == serial")
     assert torch.equal(w[0], ref) and torch.equal(w[1], ref)
     assert torch.equal(y, cz.decode(ref, shape, x.dtype, mb))
     print(json.dumps(res))
