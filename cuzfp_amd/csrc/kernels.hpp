@@ -20,7 +20,6 @@
 // Instantiated per scalar type in inst_{f32,f64,i32,i64}.hip (parallel build).
 #pragma once
 #include <hip/hip_runtime.h>
-#include <stdio.h>
 #include <stdlib.h>
 
 #include <atomic>
@@ -1662,31 +1661,14 @@ int launch_decode_encode_type(const Problem& p, const uint64_t* dstream, void* d
   if (lds + kChunkLutBytes > lds_cap_bytes()) return CUZFP_ERROR_INVALID_ARGUMENT;
   const uint32_t groups = (nwaves + kDecWaves - 1) / kDecWaves;
   const dim3 grid(2 * groups), block(kLanes * kDecWaves);
-  // each half keeps the schedule its own launcher would pick
   constexpr int occ = occupancy<Scalar, 3>::value;
-  bool dprio = use_priority(nwaves, occ, (sizeof(Scalar) == 8) ? 1 : 2);
-  bool eprio = use_priority(nwaves, occupancy<Scalar, 3, true>::value, CUZFP_ENC_PRIO_ROUNDS);
-  // (A/B: CUZFP_PIPE_PRIO = two digits, decoder then encoder half, 0/1 each)
-  static const int forced = [] {
-    const char* e = getenv("CUZFP_PIPE_PRIO");
-    return (e && e[0] && e[1]) ? ((e[0] == '1') << 1 | (e[1] == '1')) : -1;
-  }();
-  if (forced >= 0) {
-    dprio = forced >> 1;
-    eprio = forced & 1;
-  }
+  // each half keeps the schedule its own launcher picks (both on at 256^3:
+  // 47.1 us a round trip; decoder only 49.8, encoder only 51.1, neither 48.7,
+  // profiles/r05_pipeline_fused_prio.txt)
+  const bool dprio = use_priority(nwaves, occ, (sizeof(Scalar) == 8) ? 1 : 2);
+  const bool eprio = use_priority(nwaves, occupancy<Scalar, 3, true>::value, CUZFP_ENC_PRIO_ROUNDS);
   Scalar* dd = (Scalar*)ddata;
   const Scalar* ed = (const Scalar*)edata;
-  if (getenv("CUZFP_PIPE_OCC")) {  // (A/B: workgroups a CU can hold, once a process)
-    static bool said = false;
-    int nb = -1;
-    if (!said && hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                     &nb, reinterpret_cast<const void*>(&zfp_decode_encode<Scalar, 3, true, true>), (int)block.x,
-                     lds) == hipSuccess)
-      fprintf(stderr, "zfp_decode_encode: %d workgroups a CU (dynamic LDS %zu B + %zu static)\n", nb, lds,
-              (size_t)kChunkLutBytes);
-    said = true;
-  }
   if (dprio && eprio)
     hipLaunchKernelGGL((zfp_decode_encode<Scalar, 3, true, true>), grid, block, lds, st, dstream, gd, dd, ed, ge, estream, groups);
   else if (dprio)
