@@ -35,9 +35,11 @@ Prints one JSON line on rank 0 (the driver contract), with
                 copy kernel) and torch's copy_, at 1 GiB and at the input size
   host_path   = the pinned host pipeline's rates and the bare pinned H2D/D2H
                 link rates measured in the same run.
-  pipelined   = a side line, not `value`: K round trips through the
-                pipelined-batch launch (cuzfp_hip_decode_encode), checked
-                equal to the separate calls' results.
+  configs     = BASELINE configs[2] (3D f64 256^3 rate 16) and configs[3] (2D
+                f32 8192^2 rate 2) at N=1: graph-timed step GB/s, encode_ms /
+                decode_ms, the dominant kernel's roofline and the stream and
+                decoded-array SHA-256 against the reference's; timed right
+                after the headline's timed region (never part of `value`).
 """
 from __future__ import annotations
 
@@ -84,6 +86,9 @@ def parse():
                    help="GPU time each per-kernel measurement (encode_ms, decode_ms) runs for, back to back just "
                         "before the warmup steps")
     p.add_argument("--no-config5", action="store_true", help="skip BASELINE configs[4] (1024^3 sharded)")
+    p.add_argument("--no-configs", action="store_true",
+                   help="skip the records of BASELINE configs[2] (3D f64 256^3 r16) and configs[3] (2D f32 8192^2 r2) "
+                        "that the N=1 headline run times after its timed region")
     p.add_argument("--config5-edge", type=int, default=1024, help="edge of configs[4]'s global array")
     p.add_argument("--config5-steps", type=int, default=10)
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
@@ -435,6 +440,111 @@ def finish_config5(st: dict, world: int, rank: int, dev, dist) -> dict:
     return out
 
 
+OTHER_CONFIGS = (  # BASELINE configs[2], configs[3]: (workload, golden key, dims, edge, dtype, rate)
+    ("3d_float64_256^3_rate16", "baseline/3d_f64_256_r16/polynomial", 3, 256, "float64", 16.0),
+    ("2d_float32_8192^2_rate2", "baseline/2d_f32_8192_r2/polynomial", 2, 8192, "float32", 2.0),
+)
+
+
+def run_other_configs(dev, graphed, stream, steps: int = 20):
+    """BASELINE configs[2] (3D f64 256^3 rate 16) and configs[3] (2D f32 8192^2
+    rate 2), N=1, GPU phase, right after the headline's timed region: each one's
+    encode+decode step timed over `steps` steps replayed from one hipGraph (HIP
+    events on the launch stream, after ~50 ms of replays), each kernel's mean
+    duration (hipGraphs of 20 launches), the dominant kernel's roofline.  Parity
+    (stream and decoded SHA-256 against the reference's, tests/golden/golden.json)
+    is finished on the host by finish_other_configs, after the GPU work."""
+    import torch
+    import cuzfp_amd as cz
+    from cuzfp_amd.datagen import polynomial_field
+    out = []
+    for workload, key, dims, edge, dt, rate in OTHER_CONFIGS:
+        try:
+            dtype = np.dtype(dt)
+            shape = (edge,) * dims
+            a = polynomial_field(shape, dtype)
+            x = torch.from_numpy(a).to(dev)
+            del a
+            mb = cz.rate_to_maxbits(rate, dtype, dims)
+            nbs = cz.stream_bytes(shape, dtype, mb)
+            w = torch.empty(nbs // 8, dtype=torch.int64, device=dev)
+            y = torch.empty_like(x)
+
+            def step():
+                cz.encode(x, mb, out=w)
+                cz.decode(w, shape, x.dtype, mb, out=y)
+
+            run = graphed(step, steps)
+            eg = graphed(lambda: cz.encode(x, mb, out=w), 20)
+            dg = graphed(lambda: cz.decode(w, shape, x.dtype, mb, out=y), 20)
+            run()
+            torch.cuda.synchronize()
+
+            def timed(fn, count, reps):
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(reps):
+                    fn()
+                e1.record(stream)
+                torch.cuda.synchronize()
+                return e0.elapsed_time(e1) / (reps * count)
+
+            t_w = time.perf_counter()
+            while time.perf_counter() - t_w < 0.05:  # the clocks under load first
+                run()
+                torch.cuda.synchronize()
+            step_ms = timed(run, steps, 3)
+            enc_ms = timed(eg, 20, 3)
+            dec_ms = timed(dg, 20, 3)
+            run()  # leave the last step's stream and array in w, y
+            nin = x.numel() * x.element_size()
+            dom = "encode" if enc_ms >= dec_ms else "decode"
+            dom_ms = max(enc_ms, dec_ms)
+            ach = (nin + nbs) / (dom_ms * 1e-3) / 1e9
+            rec = {"workload": workload, "baseline_config": "configs[2]" if dims == 3 else "configs[3]",
+                   "shape": list(shape), "maxbits": mb, "dtype": "f64" if dt == "float64" else "f32",
+                   "GBps_input": round(nin / (step_ms * 1e-3) / 1e9, 1), "ms_per_step": round(step_ms, 4),
+                   "pct_hbm_peak": round(100.0 * 2 * (nin + nbs) / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 2),
+                   "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4),
+                   "roofline": {"bound": "hbm", "kernel": f"zfp_{dom}", "achieved": round(ach, 1),
+                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                                "algorithmic_bytes_per_launch": nin + nbs},
+                   "timing": f"{steps} steps replayed from one hipGraph x 3 (HIP events, after ~50 ms of "
+                             "replays); kernels: hipGraphs of 20 launches x 3"}
+            out.append({"record": rec, "key": key, "w": w, "y": y, "x": x})
+        except Exception as e:  # a side record never fails the bench
+            out.append({"record": {"workload": workload, "error": repr(e)[:300]}})
+    return out
+
+
+def finish_other_configs(st: list) -> list:
+    """Host-side parity of run_other_configs' last steps: the stream's and the
+    decoded array's SHA-256 against the reference zfp 0.5.0's, and the max
+    round-trip error against the reference's."""
+    import torch
+    gpath = os.path.join(ROOT, "tests", "golden", "golden.json")
+    gold = json.load(open(gpath))["cases"] if os.path.exists(gpath) else {}
+    recs = []
+    for s in st:
+        rec = s["record"]
+        if "w" in s:
+            g = gold.get(s["key"])
+            got = hashlib.sha256(s["w"].cpu().numpy().tobytes()).hexdigest()
+            dec = hashlib.sha256(s["y"].cpu().numpy().tobytes()).hexdigest()
+            err = float((s["y"].double() - s["x"].double()).abs().max().item())
+            rec["parity"] = {"stream_matches_reference": (got == g["stream_sha256"]) if g else None,
+                             "decoded_matches_reference": (dec == g["decoded_sha256"]) if g else None,
+                             "max_abs_err": err,
+                             "max_abs_err_matches_reference": (err == g["max_abs_err"]) if g else None,
+                             "golden_case": s["key"]}
+            rec["parity_ok"] = bool(g) and got == g["stream_sha256"] and dec == g["decoded_sha256"]
+        recs.append(rec)
+        s.clear()
+    torch.cuda.empty_cache()
+    return recs
+
+
 def main():
     args = parse()
     import torch
@@ -666,6 +776,13 @@ def main():
     elapsed = float(t_local.item())
     gpu_ms_per_step = ev0.elapsed_time(ev1) / args.steps
 
+    # BASELINE configs[2] and configs[3] (N=1, headline run only), on the GPU
+    # right after the timed region; their hashes with the other host checks
+    others = None
+    if (world == 1 and not strong and not args.no_configs and dims == 3 and args.dtype == "float32"
+            and n == 256 and args.rate == 8.0 and args.field == "polynomial"):
+        others = run_other_configs(dev, graphed, stream)
+
     # host-side checks, after the timed region: the stream's SHA-256 against the
     # reference's (N=1; the timed steps rewrote the same words), configs[4]'s parity
     parity = None
@@ -684,56 +801,10 @@ def main():
                 parity = "MISMATCH (decoded array)"
             else:
                 parity = "stream and decoded sha256 == reference zfp 0.5.0"
-    # Side line, outside the timed region and not `value`: K round trips through
-    # the pipelined-batch launch (cuzfp_hip_decode_encode: encode 0, then decode
-    # k with encode k+1 in one launch over two stream buffers, then decode K-1),
-    # whose results equal the separate calls'.  3D f32 at N=1 only.
-    pipelined = None
-    if world == 1 and dims == 3 and args.dtype == "float32" and not args.no_graph:
-        try:
-            words_ref = words.clone()
-            y_ref = y.clone()
-            w2 = [words, torch.empty_like(words)]
-            K = args.steps
-
-            def pipe():
-                cz.encode(x, maxbits, out=w2[0])
-                for k in range(K - 1):
-                    cz.decode_encode(w2[k & 1], y, x, w2[(k + 1) & 1], maxbits)
-                cz.decode(w2[(K - 1) & 1], shape, x.dtype, maxbits, out=y)
-
-            prun = graphed(pipe, 1)
-            prun()
-            torch.cuda.synchronize()
-            same = bool(torch.equal(w2[0], words_ref) and torch.equal(w2[1], words_ref) and torch.equal(y, y_ref))
-            # back to back for ~100 ms first (the host checks above left the GPU
-            # idle; its clocks come back under load), then 5 x 3 replays
-            t_w = time.perf_counter()
-            while time.perf_counter() - t_w < 0.1:
-                prun()
-                torch.cuda.synchronize()
-            pts = []
-            for _ in range(5):
-                p0 = torch.cuda.Event(enable_timing=True)
-                p1 = torch.cuda.Event(enable_timing=True)
-                p0.record(stream)
-                for _ in range(3):
-                    prun()
-                p1.record(stream)
-                torch.cuda.synchronize()
-                pts.append(p0.elapsed_time(p1) / (3 * K))
-            p_ms = sorted(pts)[2]
-            pipelined = {"what": "K round trips as encode 0, K-1 decode_encode launches (decode k + encode k+1), "
-                                 "decode K-1; two stream buffers; hipGraph; after ~100 ms of replays, median of 5 x 3 replays; not the headline step "
-                                 "(the reference makes separate compress / decompress calls)",
-                         "ms_per_round_trip": round(p_ms, 4), "GBps_input": round(a.nbytes / (p_ms * 1e-3) / 1e9, 1),
-                         "vs_gpu_ms_per_step": round(gpu_ms_per_step / p_ms, 4), "equal_to_separate_calls": same}
-            del w2
-        except Exception as e:  # a side line never fails the bench
-            pipelined = {"error": repr(e)[:300]}
     config5 = None
     if c5 is not None:
         config5 = c5 if "error" in c5 else finish_config5(c5, world, rank, dev, dist)
+    configs = finish_other_configs(others) if others is not None else None
 
     n_in = a.nbytes
     value = n_in * world * args.steps / elapsed / 1e9
@@ -852,8 +923,8 @@ def main():
             "cpu_baseline": cpu,
             "host_path": host_path,
             "allgather": allgather,
-            "pipelined": pipelined,
             "config5": config5,
+            "configs": configs,
             "max_abs_err": max_err,
             "parity": parity,
             "pre_timed_gpu_work": pre_timed,

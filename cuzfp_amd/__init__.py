@@ -81,8 +81,6 @@ def library() -> ctypes.CDLL:
     lib.cuzfp_hip_compress_host.argtypes = [vp, i, u, u, u, u, vp, sz, ctypes.POINTER(sz), i]
     lib.cuzfp_hip_decompress_host.restype = i
     lib.cuzfp_hip_decompress_host.argtypes = [vp, sz, i, u, u, u, u, vp, i]
-    lib.cuzfp_hip_decode_encode.restype = i
-    lib.cuzfp_hip_decode_encode.argtypes = [vp, sz, vp, vp, vp, sz, i, u, u, u, u, vp]
     lib.cuzfp_hip_copy.restype = i
     lib.cuzfp_hip_copy.argtypes = [vp, vp, sz, vp]
     lib.cuzfp_hip_release_host_cache.restype = i
@@ -221,30 +219,6 @@ def decode(words, shape, dtype, maxbits: int, out=None, stream=None):
                                     _stream_handle(stream))
     _check("decode", rc)
     return out
-
-
-def decode_encode(words_in, y, x, words_out, maxbits: int, stream=None):
-    """Decode `words_in` into `y` and encode `x` into `words_out` in one launch
-    (cuzfp_hip_decode_encode): the results of decode() and encode(), bit for
-    bit, with the encoder's waves starting in the slots the decoder's free.
-    x and y: contiguous 3D float32 tensors of one shape; the four buffers must
-    not overlap.  Raises CodecError (UNSUPPORTED_TYPE) where the combined
-    kernel does not apply; call decode() and encode() there."""
-    for t, what in ((words_in, "words_in"), (y, "y"), (x, "x"), (words_out, "words_out")):
-        if not t.is_cuda:
-            raise ValueError(f"decode_encode: {what} must be a device tensor")
-    if tuple(x.shape) != tuple(y.shape) or x.dtype != y.dtype:
-        raise ValueError("decode_encode: x and y must have one shape and dtype")
-    if not (x.is_contiguous() and y.is_contiguous()):
-        raise ValueError("decode_encode: x and y must be contiguous")
-    t = type_code(x.dtype)
-    nx, ny, nz = _extents(x.shape)
-    rc = library().cuzfp_hip_decode_encode(words_in.data_ptr(), words_in.numel() * words_in.element_size(),
-                                           y.data_ptr(), x.data_ptr(), words_out.data_ptr(),
-                                           words_out.numel() * words_out.element_size(), t, nx, ny, nz,
-                                           maxbits, _stream_handle(stream))
-    _check("decode_encode", rc)
-    return y, words_out
 
 
 def copy(src, dst, stream=None):

@@ -416,6 +416,9 @@ static hipError_t pick_copy_queues(PipelineCache& r) {
       }
     }
   }
+  // nothing of a failed trial may still use the buffers when they are freed
+  if (e != hipSuccess)
+    for (int q = 0; q < kPickStreams; q++) (void)hipStreamSynchronize(r.st[q]);
   for (int i = 0; i < 2 * kChunks; i++)
     if (ev[i]) (void)hipEventDestroy(ev[i]);
   (void)hipFree(d);
@@ -539,7 +542,16 @@ static int host_pipeline(const Problem& p, bool encode, void* h_data, void* h_st
     CUZFP_HIP_TRY(hipEventCreateWithFlags(&r.ev_done[i], hipEventDisableTiming));
     r.nst = i + 1;
   }
-  if (ordered && !r.queues_picked) CUZFP_HIP_TRY(pick_copy_queues(r));
+  if (ordered && !r.queues_picked && pick_copy_queues(r) != hipSuccess) {
+    // The calibration only tunes which streams carry the copies: if it cannot
+    // run (e.g. its 24 MiB of pinned and device memory are not available),
+    // clear the error, keep the default roles and do not retry every call.
+    (void)hipGetLastError();
+    r.q_in = 0;
+    r.q_k = 1;
+    r.q_out = 2;
+    r.queues_picked = true;
+  }
   CallHostBuf pin_in[kMaxStreams], pin_out[kMaxStreams];
   for (int i = 0; i < S; i++) {
     if (!in_pinned) CUZFP_HIP_TRY(pin_in[i].get(r.pin_in[i], max_in));
@@ -786,20 +798,6 @@ int cuzfp_hip_decode(const uint64_t* d_stream, size_t stream_bytes, int type, un
   if (!d_data || !d_stream) return CUZFP_ERROR_INVALID_ARGUMENT;
   if (stream_bytes < stream_bytes_of(p.g)) return CUZFP_ERROR_BUFFER_TOO_SMALL;
   return launch_decode(p, d_stream, d_data, 0, waves_of(p.g), stream);
-}
-
-int cuzfp_hip_decode_encode(const uint64_t* d_stream_in, size_t stream_bytes, void* d_data_out,
-                            const void* d_data_in, uint64_t* d_stream_out, size_t stream_capacity,
-                            int type, unsigned nx, unsigned ny, unsigned nz, unsigned maxbits,
-                            hipStream_t stream) {
-  Problem p;
-  int rc = make_problem(type, nx, ny, nz, 0, 0, 0, maxbits, &p);
-  if (rc) return rc;
-  if (!d_stream_in || !d_data_out || !d_data_in || !d_stream_out) return CUZFP_ERROR_INVALID_ARGUMENT;
-  const size_t need = stream_bytes_of(p.g);
-  if (stream_bytes < need || stream_capacity < need) return CUZFP_ERROR_BUFFER_TOO_SMALL;
-  if (type != CUZFP_TYPE_FLOAT) return CUZFP_ERROR_UNSUPPORTED_TYPE;
-  return launch_decode_encode_type<float>(p, d_stream_in, d_data_out, d_data_in, d_stream_out, stream);
 }
 
 int cuzfp_hip_copy(const void* d_src, void* d_dst, size_t bytes, hipStream_t stream) {

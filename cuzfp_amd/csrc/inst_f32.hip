@@ -6,10 +6,6 @@ template int launch_encode_type<float>(const Problem&, const void*, bool, uint64
                                        uint32_t, hipStream_t);
 template int launch_decode_type<float>(const Problem&, const uint64_t*, bool, void*, uint32_t,
                                        uint32_t, hipStream_t);
-#if !defined(CUZFP_XVAR)
-template int launch_decode_encode_type<float>(const Problem&, const uint64_t*, void*, const void*, uint64_t*,
-                                              hipStream_t);
-#endif
 }  // namespace cuzfp
 
 #if defined(CUZFP_PROBE) && CUZFP_PROBE == 9

@@ -990,7 +990,7 @@ __device__ __forceinline__ void zfp_encode_body(const Scalar* __restrict__ data,
 }
 
 // The kernel: the body above for workgroup blockIdx.x, with its tables in the
-// kernel's static LDS (zfp_decode_encode runs the same body for part of its grid).
+// kernel's static LDS.
 template <typename Scalar, int DIMS, bool FAST, bool ALIGNED, bool PRIO = true, int REG = 0, int WPG = kEncWaves>
 __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS, true>::value)) void zfp_encode(const Scalar* __restrict__ data,
                                                                       Geometry g,
@@ -1207,7 +1207,7 @@ __device__ __forceinline__ void zfp_decode_body(const uint64_t* __restrict__ str
 }
 
 // The kernel: the body above for workgroup blockIdx.x, with its tables in the
-// kernel's static LDS (zfp_decode_encode runs the same body for part of its grid).
+// kernel's static LDS.
 template <typename Scalar, int DIMS, bool FAST, bool PRIO = true, int REG = 0, int WPG = kDecWaves>
 __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) void zfp_decode(const uint64_t* __restrict__ stream,
                                                                       Geometry g,
@@ -1216,30 +1216,6 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) voi
   // 1D: the plane table (Plane1dDecLut, 16 KiB)
   __shared__ __attribute__((aligned(16))) uint16_t dtab[DIMS == 1 ? sizeof(Plane1dDecLut) / 2 : 8];
   zfp_decode_body<Scalar, DIMS, FAST, PRIO, REG, WPG>(stream, g, data, blockIdx.x, ctab, dtab);
-}
-
-// Two batches in one launch (cuzfp_hip_decode_encode; no reference
-// counterpart, the reference serialises compress and decompress calls):
-// workgroups [0, dgroups) decode one stream into an array, the rest encode
-// another array into a second stream.  The dispatcher places workgroups in
-// order, so every decode workgroup starts first and the encode workgroups take
-// the slots the decoder's waves free as they finish: the encoder's loads
-// overlap the decoder's last planes and its output writes, which one resident
-// round of each kernel (256^3) cannot do.  One static LDS region holds either
-// half's tables at address 0 (the chunk tables, 12 KiB; the spread tables use
-// its first 2 KiB), so a workgroup needs the tables once.
-template <typename Scalar, int DIMS, bool DPRIO, bool EPRIO>
-__global__ __launch_bounds__(kLanes * kDecWaves, (occupancy<Scalar, DIMS>::value)) void zfp_decode_encode(
-    const uint64_t* __restrict__ dstream, Geometry gd, Scalar* __restrict__ ddata,
-    const Scalar* __restrict__ edata, Geometry ge, uint64_t* __restrict__ estream, uint32_t dgroups) {
-  static_assert(kDecWaves == kEncWaves, "one workgroup shape for both halves");
-  static_assert(occupancy<Scalar, DIMS>::value == occupancy<Scalar, DIMS, true>::value, "one register budget");
-  static_assert(kChunkLutBytes >= kSpreadTabBytes, "the spread tables fit the chunk tables' region");
-  __shared__ __attribute__((aligned(16))) uint32_t tabs[kChunkLutBytes / 4];  // LDS address 0 (static)
-  if (blockIdx.x < dgroups)
-    zfp_decode_body<Scalar, DIMS, true, DPRIO, 0, kDecWaves>(dstream, gd, ddata, blockIdx.x, tabs, (uint16_t*)tabs);
-  else
-    zfp_encode_body<Scalar, DIMS, true, true, EPRIO, 0, kEncWaves>(edata, ge, estream, blockIdx.x - dgroups, tabs, tabs);
 }
 
 // The register-writer encoder (1D/2D, maxbits 32 / 64) with K batches of 64
@@ -1630,57 +1606,6 @@ int launch_decode_type(const Problem& p, const uint64_t* stream, bool fast, void
   }
 }
 
-// zfp_decode_encode for a 3D field on the fast paths (contiguous, 16-byte
-// aligned arrays, extents multiples of 4, maxbits a multiple of 64): the two
-// halves' geometries as launch_decode_t / launch_encode_t build them.
-// CUZFP_ERROR_UNSUPPORTED_TYPE for anything else (the caller launches the two
-// kernels), CUZFP_ERROR_INVALID_ARGUMENT when the shared layout does not fit
-// the workgroup's LDS.
-template <typename Scalar>
-int launch_decode_encode_type(const Problem& p, const uint64_t* dstream, void* ddata, const void* edata,
-                              uint64_t* estream, hipStream_t st) {
-  const Geometry& g = p.g;
-  if (p.dims != 3 || !p.fast_ok || (g.maxbits & 63) || ((uintptr_t)ddata & 15) || ((uintptr_t)edata & 15))
-    return CUZFP_ERROR_UNSUPPORTED_TYPE;
-  const uint32_t nwaves = (g.nblocks + kLanes - 1) / kLanes;
-  if (!nwaves) return CUZFP_SUCCESS;
-  Geometry gd = g, ge = g;
-  gd.wave0 = ge.wave0 = 0;
-  gd.wave_end = ge.wave_end = nwaves;
-  gd.vec_io = (g.maxbits % 2 == 0) && ((uintptr_t)dstream % 16 == 0);
-  ge.vec_io = (g.maxbits % 2 == 0) && ((uintptr_t)estream % 16 == 0);
-  gd.lds_words = ((g.maxbits + 31) / 32 + 5) * 32;
-  ge.lds_words = g.maxbits + kLanes * kSlackWords;
-  gd.row_stage = ge.row_stage = 0;
-  if (sizeof(Scalar) == 8 && g.bx % kLanes == 0) {
-    const size_t img = (size_t)gd.lds_words * 8;
-    gd.row_stage = img >= 4 * 2048 ? 4 : img >= 2 * 2048 ? 2 : img >= 2048 ? 1 : 0;
-  }
-  const uint32_t words = gd.lds_words > ge.lds_words ? gd.lds_words : ge.lds_words;
-  const size_t lds = (size_t)kDecWaves * words * 8;
-  if (lds + kChunkLutBytes > lds_cap_bytes()) return CUZFP_ERROR_INVALID_ARGUMENT;
-  const uint32_t groups = (nwaves + kDecWaves - 1) / kDecWaves;
-  const dim3 grid(2 * groups), block(kLanes * kDecWaves);
-  constexpr int occ = occupancy<Scalar, 3>::value;
-  // each half keeps the schedule its own launcher picks (both on at 256^3:
-  // 47.1 us a round trip; decoder only 49.8, encoder only 51.1, neither 48.7,
-  // profiles/r05_pipeline_fused_prio.txt)
-  const bool dprio = use_priority(nwaves, occ, (sizeof(Scalar) == 8) ? 1 : 2);
-  const bool eprio = use_priority(nwaves, occupancy<Scalar, 3, true>::value, CUZFP_ENC_PRIO_ROUNDS);
-  Scalar* dd = (Scalar*)ddata;
-  const Scalar* ed = (const Scalar*)edata;
-  if (dprio && eprio)
-    hipLaunchKernelGGL((zfp_decode_encode<Scalar, 3, true, true>), grid, block, lds, st, dstream, gd, dd, ed, ge, estream, groups);
-  else if (dprio)
-    hipLaunchKernelGGL((zfp_decode_encode<Scalar, 3, true, false>), grid, block, lds, st, dstream, gd, dd, ed, ge, estream, groups);
-  else if (eprio)
-    hipLaunchKernelGGL((zfp_decode_encode<Scalar, 3, false, true>), grid, block, lds, st, dstream, gd, dd, ed, ge, estream, groups);
-  else
-    hipLaunchKernelGGL((zfp_decode_encode<Scalar, 3, false, false>), grid, block, lds, st, dstream, gd, dd, ed, ge, estream, groups);
-  const hipError_t e = hipGetLastError();
-  t_last_hip = e;
-  return e == hipSuccess ? CUZFP_SUCCESS : CUZFP_ERROR_HIP;
-}
 #endif
 
 }  // namespace cuzfp

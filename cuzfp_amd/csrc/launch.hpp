@@ -56,8 +56,5 @@ int launch_encode_type(const Problem& p, const void* data, bool fast, uint64_t* 
 template <typename Scalar>
 int launch_decode_type(const Problem& p, const uint64_t* stream, bool fast, void* data,
                        uint32_t wave0, uint32_t nwaves, hipStream_t st);
-template <typename Scalar>
-int launch_decode_encode_type(const Problem& p, const uint64_t* dstream, void* ddata, const void* edata,
-                              uint64_t* estream, hipStream_t st);
 
 }  // namespace cuzfp

@@ -111,21 +111,6 @@ int cuzfp_hip_decode(const uint64_t* d_stream, size_t stream_bytes, int type, un
                      unsigned ny, unsigned nz, long long sx, long long sy, long long sz,
                      unsigned maxbits, void* d_data, hipStream_t stream);
 
-/* Two independent batches in one launch (no reference counterpart: the
- * reference serialises cuZFP::compress and cuZFP::decompress calls,
- * ref:cuZFP/cuZFP.cu:174-269): decode d_stream_in into d_data_out and encode
- * d_data_in into d_stream_out, both fields of the same shape and maxbits,
- * contiguous.  The results are those of cuzfp_hip_decode and cuzfp_hip_encode
- * (bit for bit); the launch lets the encoder's waves start in the slots the
- * decoder's waves free, so a stream of round trips can run encode k+1 beside
- * decode k.  The four buffers must not overlap.  CUZFP_ERROR_UNSUPPORTED_TYPE
- * where the combined kernel does not apply (3D float32 on the fast paths with
- * maxbits a multiple of 64, 16-byte aligned arrays): call the two functions. */
-int cuzfp_hip_decode_encode(const uint64_t* d_stream_in, size_t stream_bytes, void* d_data_out,
-                            const void* d_data_in, uint64_t* d_stream_out, size_t stream_capacity,
-                            int type, unsigned nx, unsigned ny, unsigned nz, unsigned maxbits,
-                            hipStream_t stream);
-
 /* Host-memory end to end: the array and the stream live in
  * host memory; the library moves them in z-slab (3D) / y-slab (2D) / x-range
  * (1D) chunks on three HIP streams -- input copies, kernels, output copies,

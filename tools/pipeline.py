@@ -80,14 +80,7 @@ def main():
             fn()
         return g.replay
 
-    def fused():
-        # E_0; then decode k and encode k+1 in one launch; D_{K-1}
-        cz.encode(x, mb, out=w[0])
-        for k in range(K - 1):
-            cz.decode_encode(w[k & 1], y, x, w[(k + 1) & 1], mb)
-        cz.decode(w[(K - 1) & 1], shape, x.dtype, mb, out=y)
-
-    variants = {"serial": graphed(serial), "fused": graphed(fused), "fused-eager": fused, "pipe-eager": pipelined,
+    variants = {"serial": graphed(serial), "pipe-eager": pipelined,
                 "pipe-prio-dec": lambda: pipelined_on(lo, hi),
                 "pipe-prio-enc": lambda: pipelined_on(hi2, lo2)}
     if a.only:
@@ -114,16 +107,13 @@ def main():
         res[name] = round(sorted(r)[3], 2)
         print(f"{name:11s} {res[name]:8.2f} us per round trip", flush=True)
     # the pipelined round trips decode to the same array
-    for f in (pipelined_on, None):
+    for f in (pipelined_on,):
         w[0].zero_(); w[1].zero_(); y.zero_()
-        if f is None:
-            fused()
-        else:
-            f(lo, hi)
+        f(lo, hi)
         torch.cuda.synchronize()
         assert torch.equal(w[0], ref) and torch.equal(w[1], ref)
         assert torch.equal(y, cz.decode(ref, shape, x.dtype, mb))
-    print("pipelined and fused round trips: streams and decode == serial")
+    print("pipelined round trips: streams and decode == serial")
     assert torch.equal(w[0], ref) and torch.equal(w[1], ref)
     assert torch.equal(y, cz.decode(ref, shape, x.dtype, mb))
     print(json.dumps(res))
