@@ -283,7 +283,6 @@ struct LdsReader {
   const uint16_t* d1d;    // 1D: the workgroup's plane table (Plane1dDecLut)
   uint32_t pos;
   uint32_t end;  // the block's budget end (decode_planes sets it; pos never passes it)
-  uint32_t rare_lim;  // kNotEnded - 1, held in an SGPR (decode_planes sets it)
   uint32_t x0, x1, x2, x3, x4;
   // byte address of the row holding bit p: lds32 + 256 * (p >> 5), in two
   // instructions (the compiler's form of the same expression takes three)
@@ -345,12 +344,12 @@ struct LdsReader {
   // to zero for lanes whose leading test is "0" -- entry 0, a broadcast --
   // cut the LDS bank-conflict cycles, but its two VALU a plane cost more:
   // 256^3 r8 decode 23.5 -> 23.2 us without it, tools/xvar.py, r04_nolead.)
-  // byte offsets of chunk 1's state-2 entry (chunk bits 0-9; the state-2
-  // table is at LDS address 0) and of chunk 2's pair of state-0/1 entries
-  // (bits 10-19; from the pair table's start, kLutPairs)
+  // byte offsets of chunk 1's state-2 entry and selector (chunk bits 0-9;
+  // 8-byte entries, the table at LDS address 0) and of chunk 2's pair of
+  // state-0/1 entries (bits 10-19; from the pair table's start, kLutPairs)
   static __device__ __forceinline__ uint32_t off1(uint32_t gm) {
     uint32_t a;
-    asm("v_lshlrev_b32 %0, 2, %1\n\tv_and_b32 %0, 0xffc, %0" : "=&v"(a) : "v"(gm));
+    asm("v_lshlrev_b32 %0, 3, %1\n\tv_and_b32 %0, 0x1ff8, %0" : "=&v"(a) : "v"(gm));
     return a;
   }
   static __device__ __forceinline__ uint32_t off2(uint32_t gm) {
@@ -364,12 +363,15 @@ struct LdsReader {
     const uint64_t v = *(lds_u64*)((uintptr_t)(lds_u32*)lut32 + byte_off);
     return uint2{(uint32_t)v, (uint32_t)(v >> 32)};
   }
-  // the table steps' lookups: entry (2, g's chunk 1) and the pair (0, chunk 2),
-  // (1, chunk 2) in one ds_read_b64.  (With n = N-1 the group part is the last
-  // position's bit alone; the parse then runs past position N-1, which the
-  // steps' implied-one rule resolves.)
-  __device__ __forceinline__ void chunks_fast(uint32_t g, uint32_t& e1, uint32_t& e2a, uint32_t& e2b) const {
-    e1 = tab(off1(g));
+  // the table steps' lookups: entry (2, g's chunk 1) with its chunk-2
+  // selector, and the pair (0, chunk 2), (1, chunk 2), each one ds_read_b64.
+  // (With n = N-1 the group part is the last position's bit alone; the parse
+  // then runs past position N-1, which the steps' implied-one rule resolves.)
+  __device__ __forceinline__ void chunks_fast(uint32_t g, uint32_t& e1, uint32_t& sel, uint32_t& e2a,
+                                              uint32_t& e2b) const {
+    const uint2 c = tab64(off1(g));
+    e1 = c.x;
+    sel = c.y;
     const uint2 p = tab64(kPairBytes + off2(g));
     e2a = p.x;
     e2b = p.y;
@@ -434,15 +436,15 @@ struct LdsReader {
 // < 16), so a window is one 64-bit shift of the zero-extended block, without
 // the bounds test and selects a block of up to 64 bits needs (five of the
 // plane step's slow-issue VALU instructions).
-// B32 also keeps the block shifted up by 2 (blk4): the group window is taken
-// from it, so a chunk's 10 bits sit at bits 2-11, already a byte offset of
-// the 4-byte entries (one AND instead of a shift and an AND).
+// B32 also keeps the block shifted up by 3 (blk8): the group window is taken
+// from it, so a chunk's 10 bits sit at bits 3-12, already a byte offset of
+// chunk 1's 8-byte entries (one AND instead of a shift and an AND).
 template <bool PRIO = true, bool B32 = false>
 struct RegReader : LdsReader<PRIO> {
-  uint64_t blk, blk4;
+  uint64_t blk, blk8;
   __device__ __forceinline__ void set_block(uint64_t b) {
     blk = b;
-    if constexpr (B32) blk4 = b << 2;
+    if constexpr (B32) blk8 = b << 3;
   }
   __device__ __forceinline__ uint64_t at(uint32_t p) const {
     if constexpr (B32) return blk >> p;
@@ -451,35 +453,38 @@ struct RegReader : LdsReader<PRIO> {
   __device__ __forceinline__ void windows(uint32_t m, uint64_t& w, uint32_t& g) const {
     w = at(this->pos);
     if constexpr (B32)
-      g = (uint32_t)(blk4 >> (this->pos + m));  // the group window << 2
+      g = (uint32_t)(blk8 >> (this->pos + m));  // the group window << 3
     else
       g = (uint32_t)at(this->pos + m);
   }
   __device__ __forceinline__ uint32_t window_g(uint32_t m, WRaw& wr) const {
     wr = WRaw{0u, 0u, 0u};
-    if constexpr (B32) return (uint32_t)(blk4 >> (this->pos + m));  // the group window << 2
+    if constexpr (B32) return (uint32_t)(blk8 >> (this->pos + m));  // the group window << 3
     return (uint32_t)at(this->pos + m);
   }
   __device__ __forceinline__ uint64_t window_w_make(const WRaw&) const { return at(this->pos); }
-  // (B32: g from windows() is the group window << 2; its bit 2 is the leading
+  // (B32: g from windows() is the group window << 3; its bit 3 is the leading
   // test)
-  __device__ __forceinline__ void chunks_fast(uint32_t g, uint32_t& e1, uint32_t& e2a, uint32_t& e2b) const {
+  __device__ __forceinline__ void chunks_fast(uint32_t g, uint32_t& e1, uint32_t& sel, uint32_t& e2a,
+                                              uint32_t& e2b) const {
     if constexpr (B32) {
       // (no lead mask here: at 8 waves a SIMD the 2D decoder's LDS is not
       // what it waits on, and the mask's two VALU a plane are)
-      e1 = this->tab(g & 0xffcu);
-      const uint2 p = this->tab64(LdsReader<PRIO>::kPairBytes + ((g >> 9) & 0x1ff8u));
+      const uint2 c = this->tab64(g & 0x1ff8u);
+      e1 = c.x;
+      sel = c.y;
+      const uint2 p = this->tab64(LdsReader<PRIO>::kPairBytes + ((g >> 10) & 0x1ff8u));
       e2a = p.x;
       e2b = p.y;
     } else {
-      LdsReader<PRIO>::chunks_fast(g, e1, e2a, e2b);
+      LdsReader<PRIO>::chunks_fast(g, e1, sel, e2a, e2b);
     }
   }
   __device__ __forceinline__ uint32_t chunk1_fast(uint32_t g) const {
     if constexpr (B32) {
       uint32_t t;
-      asm("v_bfe_i32 %0, %1, 2, 1" : "=v"(t) : "v"(g));
-      return this->tab((g & t) & 0xffcu);
+      asm("v_bfe_i32 %0, %1, 3, 1" : "=v"(t) : "v"(g));
+      return this->tab((g & t) & 0x1ff8u);
     } else {
       return LdsReader<PRIO>::chunk1_fast(g);
     }
@@ -877,7 +882,13 @@ __device__ __forceinline__ void zfp_encode_body(const Scalar* __restrict__ data,
   // slower, round 4: 256^3 r16 encode 51.1 -> 54.5 us with non-temporal
   // loads, 50.9 -> 54.4 us with plain ones; non-temporal hints on these
   // strided row loads: 50.9 -> 55.6 us)
-  if (b < g.nblocks) {
+  // A wave of live blocks only (every wave but a partial last one) gathers
+  // behind one wave-uniform test: with the per-lane test alone the compiler
+  // zeroes the whole block first (64 v_mov a wave, on every wave) and then
+  // loads over it under the lane mask.
+  if ((wave + 1) * kLanes <= g.nblocks) {
+    gather<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
+  } else if (b < g.nblocks) {
     gather<Scalar, DIMS, FAST>(data, g, block_pos<DIMS>(g, b), f);
   } else if constexpr (ALIGNED && !REG) {
     // a lane past the last block codes a zero block (see below)

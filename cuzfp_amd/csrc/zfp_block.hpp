@@ -1389,22 +1389,31 @@ ZFP_HD PW decode_plane(unsigned& bits, unsigned& n, Reader& rd) {
 // grammar (decode.c:302-317 read the same grammar bit by bit).
 constexpr int kChunkBits = 10;
 constexpr uint32_t kChunkMask = (1u << kChunkBits) - 1;
-// entry: bits used U [0,14) | 0 | ones [15,25) | positions covered [26,31) |
-// exit state bit 31.  The fields have room for the sum of two entries (ones
-// < 2^11, positions <= 20 < 2^5, U wraps into the zero bit), so one add
-// combines chunk 1 and chunk 2.  U also says whether the code ended, by a
-// marker M = 2^13 (larger than any budget, maxbits <= 8000): a chunk-1 entry
-// that did not end carries M, a chunk-2 entry that did end carries M too, so
-// the sum's U holds M (mod 2^14) exactly when the code has not ended -- and
-// one compare against the budget rejects both a code running past the budget
-// and one longer than two chunks.
-constexpr unsigned kOnesShift = 15, kPosShift = 26;
-constexpr uint32_t kUsedMask = (1u << 14) - 1, kNotEnded = 1u << 13;
-constexpr uint32_t kEntryState = 1u << 31;
+// entry (one dword): ones [0,10) | 0 | positions covered [11,16) | exit state
+// bit 16 | 0 | bits used U [18,32).  The fields have room for the sum of two
+// entries (ones < 2^11 and the states' sum < 4 carry into zero bits,
+// positions <= 20 < 2^5, U's carry leaves the dword), so one add combines
+// chunk 1 and chunk 2.  U also says whether the code ended, by a marker M =
+// 2^13 (U's top bit, the dword's sign bit): a chunk-1 entry that did not end
+// carries M, a chunk-2 entry that did end carries M too, so the sum's U holds
+// M (mod 2^14) exactly when the code has not ended -- the sum is negative.
+// (Round 6: the fields the common step reads sit where fast-issue
+// instructions reach them -- the ones by an AND with an inline constant, the
+// positions as a shift count taken from the low 5 bits of e >> 11, U by one
+// shift, the marker as the sign bit -- instead of behind v_bfe_u32.)
+constexpr unsigned kOnesShift = 0, kPosShift = 11, kStateShift = 16, kUsedShift = 18;
+constexpr uint32_t kNotEnded = 1u << 13;           // in U's units
+constexpr uint32_t kEntryState = 1u << kStateShift;
+constexpr uint32_t kMarkerBit = kNotEnded << kUsedShift;  // bit 31
 
 constexpr uint32_t pack_entry(uint32_t ones, uint32_t pos, uint32_t used, uint32_t flags) {
-  return (ones << kOnesShift) | (pos << kPosShift) | used | flags;
+  return (ones << kOnesShift) | (pos << kPosShift) | (used << kUsedShift) | flags;
 }
+// an entry's (or a sum's) fields
+ZFP_HD constexpr uint32_t ent_ones(uint32_t e) { return (e >> kOnesShift) & ((1u << kChunkBits) - 1u); }
+ZFP_HD constexpr uint32_t ent_pos(uint32_t e) { return (e >> kPosShift) & 31u; }
+ZFP_HD constexpr uint32_t ent_state(uint32_t e) { return (e >> kStateShift) & 1u; }
+ZFP_HD constexpr uint32_t ent_used(uint32_t e) { return e >> kUsedShift; }  // 14 bits, the marker included
 
 // state 0: at a token boundary; 1: the first bit is the pending group test of
 // a one that closed the previous chunk; 2: the first bit is the plane's
@@ -1437,22 +1446,52 @@ constexpr uint32_t chunk_entry(unsigned state, uint32_t b) {
   return pack_entry(ones, pos, kChunkBits + mark_open, 0);
 }
 
-// Table layout: state 2 (chunk 1, the leading group test first) at
-// [0, 2^B), indexed by the chunk; states 0 and 1 side by side at
-// [2^B, 2^B + 2^(B+1)), chunk b's pair at 2^B + 2b, so one ds_read_b64 reads
-// both (64 banks, one LDS instruction, where two ds_read_b32 -- or one
+// The chunk-2 entry a chunk-1 entry selects, as one v_perm_b32 of the pair
+// (e2a: state 0, e2b: state 1) by the selector stored beside chunk 1's entry:
+// bytes 0-3 (e2a) or 4-7 (e2b) by chunk 1's exit state, or 0x0c bytes (zero)
+// when chunk 1 ended the code -- one slow-class instruction where the select
+// by the exit state and the mask by the marker took four (round 6).
+constexpr uint32_t kSelState0 = 0x03020100u, kSelState1 = 0x07060504u, kSelNone = 0x0c0c0c0cu;
+constexpr uint32_t chunk_sel(uint32_t e1) {
+  return !(e1 & kMarkerBit) ? kSelNone : (e1 & kEntryState) ? kSelState1 : kSelState0;
+}
+// v_perm_b32(b, a, sel): byte i of the result is selector byte i's pick of
+// {a = bytes 0-3, b = bytes 4-7}, 0x00 for 12, 0xff for 13 and up (the
+// sign-replicating selectors 8-11 are not used here)
+ZFP_HD uint32_t perm_sel(uint32_t b, uint32_t a, uint32_t sel) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_perm(b, a, sel);
+#else
+  const uint64_t v = (uint64_t)a | ((uint64_t)b << 32);
+  uint32_t r = 0;
+  for (int i = 0; i < 4; i++) {
+    const uint32_t k = (sel >> (8 * i)) & 0xffu;
+    const uint32_t byte = k < 8 ? (uint32_t)(v >> (8 * k)) & 0xffu : k == 12 ? 0u : 0xffu;
+    r |= byte << (8 * i);
+  }
+  return r;
+#endif
+}
+
+// Table layout (16 KiB): chunk 1 (state 2, the leading group test first) at
+// dwords [0, 2^(B+1)), chunk b's entry at 2b and its chunk-2 selector at
+// 2b + 1, so one ds_read_b64 reads both; states 0 and 1 side by side at
+// [2^(B+1), 2^(B+2)), chunk b's pair at 2^(B+1) + 2b, one ds_read_b64 too (64
+// banks, one LDS instruction, where two ds_read_b32 -- or one
 // ds_read2st64_b32, served as two -- each take the 32-bank conflicts of the
-// lanes' random entries).  1D reads the state-2 table alone.
-constexpr uint32_t kLutS2 = 0, kLutPairs = 1u << kChunkBits;
-ZFP_HD constexpr uint32_t lut_s2_index(uint32_t b) { return kLutS2 + (b & kChunkMask); }
+// lanes' random entries).  1D reads the chunk-1 table alone.
+constexpr uint32_t kLutS2 = 0, kLutPairs = 2u << kChunkBits;
+ZFP_HD constexpr uint32_t lut_s2_index(uint32_t b) { return kLutS2 + 2u * (b & kChunkMask); }
 ZFP_HD constexpr uint32_t lut_pair_index(uint32_t b, uint32_t state) { return kLutPairs + 2u * (b & kChunkMask) + state; }
 struct ChunkLut {
-  uint32_t e[3u << kChunkBits];
+  uint32_t e[4u << kChunkBits];
 };
 constexpr ChunkLut make_chunk_lut() {
   ChunkLut t{};
   for (uint32_t b = 0; b <= kChunkMask; b++) {
-    t.e[lut_s2_index(b)] = chunk_entry(2, b);
+    const uint32_t e1 = chunk_entry(2, b);
+    t.e[lut_s2_index(b)] = e1;
+    t.e[lut_s2_index(b) + 1] = chunk_sel(e1);
     t.e[lut_pair_index(b, 0)] = chunk_entry(0, b);
     t.e[lut_pair_index(b, 1)] = chunk_entry(1, b);
   }
@@ -1490,36 +1529,10 @@ ZFP_HD uint32_t and_or(uint32_t a, uint32_t m, uint32_t c) {
 #endif
 }
 
-// all ones when bit B of e is set, else 0 (one v_bfe_i32)
-ZFP_HD uint32_t sbfe1(uint32_t e, int B) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  return (uint32_t)__builtin_amdgcn_sbfe((int)e, (unsigned)B, 1u);
-#else
-  return (e >> B) & 1u ? ~0u : 0u;
-#endif
-}
 
-// v when bit 13 of e is set, else 0 (v_bfe_i32 + v_and_b32)
-ZFP_HD uint32_t keep_if_bit13(uint32_t v, uint32_t e) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  uint32_t m;
-  asm("v_bfe_i32 %0, %1, 13, 1" : "=v"(m) : "v"(e));
-  return v & m;
-#else
-  return (e >> 13) & 1u ? v : 0u;
-#endif
-}
-
-// v unless bit 13 of e is set (v_bfe_i32 + v_bfi_b32)
-ZFP_HD uint32_t drop_if_bit13(uint32_t v, uint32_t e) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  uint32_t m;
-  asm("v_bfe_i32 %0, %1, 13, 1" : "=v"(m) : "v"(e));
-  return v & ~m;
-#else
-  return (e >> 13) & 1u ? 0u : v;
-#endif
-}
+// v unless e carries the marker (its sign bit): one arithmetic shift and an
+// AND-NOT, both fast-issue
+ZFP_HD uint32_t drop_if_marked(uint32_t v, uint32_t e) { return v & ~(uint32_t)((int32_t)e >> 31); }
 
 // A two-chunk parse that covers position N-1 (npos > q = N-1-n): there the
 // reference reads nothing -- its zero loop stops at N-1 and the one there is
@@ -1530,14 +1543,14 @@ ZFP_HD uint32_t drop_if_bit13(uint32_t v, uint32_t e) {
 // kChunkBits + s1 + (q - p1) + (ones before q - p1).  Returns that bit count
 // and sets `ones` to the ones below N-1 plus the implied one.
 ZFP_HD uint32_t implied_end(uint32_t e1, uint32_t e2, uint32_t q, uint64_t& ones) {
-  const uint32_t p1 = (e1 >> kPosShift) & 31u;
-  const uint32_t o1 = (e1 >> kOnesShift) & kChunkMask, o2 = (e2 >> kOnesShift) & kChunkMask;
+  const uint32_t p1 = ent_pos(e1);
+  const uint32_t o1 = ent_ones(e1), o2 = ent_ones(e2);
   uint32_t o;
   if (p1 > q) {
     o = 1u + q + (uint32_t)__builtin_popcount(o1 & ((1u << q) - 1u));
   } else {
     const uint32_t q2 = q - p1;
-    o = kChunkBits + (e1 >> 31) + q2 + (uint32_t)__builtin_popcount(o2 & ((1u << q2) - 1u));
+    o = kChunkBits + ent_state(e1) + q2 + (uint32_t)__builtin_popcount(o2 & ((1u << q2) - 1u));
   }
   ones = (ones & ((1ull << q) - 1ull)) | (1ull << q);
   return o;
@@ -1564,13 +1577,12 @@ ZFP_HD PW lut_finish(unsigned& bits, unsigned& n, Reader& rd, bool& slow, unsign
   constexpr unsigned N = 1u << (2 * DIMS);
   const unsigned b1 = bits - m;                // budget after the verbatim bits
   const uint32_t S = e1 + e2;                  // field-wise sums
-  uint32_t npos = S >> kPosShift & 31u;
-  const uint32_t used = S & kUsedMask;         // >= kNotEnded: the code has not ended
-  uint64_t ones = ((e1 >> kOnesShift) & kChunkMask) |
-                  (((e2 >> kOnesShift) & kChunkMask) << ((e1 >> kPosShift) & 31u));
+  uint32_t npos = ent_pos(S);
+  const uint32_t used = ent_used(S);           // >= kNotEnded: the code has not ended
+  uint64_t ones = ent_ones(e1) | (ent_ones(e2) << ent_pos(e1));
   bool ended = used < kNotEnded;
   uint32_t parsed = used & (kNotEnded - 1u);  // code bits read (all of the chunks' if not ended)
-  uint32_t st = (DIMS == 1 ? e1 : e2) >> 31;          // exit state of the last chunk read
+  uint32_t st = ent_state(DIMS == 1 ? e1 : e2);       // exit state of the last chunk read
   const uint32_t q = N - 1 - nf;
   // the code bits up to position N-1's token when a continuation pair reaches
   // it (the first pair's case is implied_end below)
@@ -1587,10 +1599,10 @@ ZFP_HD PW lut_finish(unsigned& bits, unsigned& n, Reader& rd, bool& slow, unsign
           const uint32_t gg = rd.window32(rd.pos + m + parsed);
           uint32_t eA, eBa, eBb;
           rd.chunks_st(gg, st, eA, eBa, eBb);
-          const uint32_t eB = drop_if_bit13((eA & kEntryState) ? eBb : eBa, eA);
+          const uint32_t eB = drop_if_marked((eA & kEntryState) ? eBb : eBa, eA);
           const uint32_t T = eA + eB;
-          const uint32_t pA = (eA >> kPosShift) & 31u;
-          const uint32_t oA = (eA >> kOnesShift) & kChunkMask, oB = (eB >> kOnesShift) & kChunkMask;
+          const uint32_t pA = ent_pos(eA);
+          const uint32_t oA = ent_ones(eA), oB = ent_ones(eB);
           const uint64_t o = oA | ((uint64_t)oB << pA);
           // this pair reaches position N-1 (offset q2 into it): the code ends
           // at the start of that position's token -- st + q2 + the ones'
@@ -1598,14 +1610,14 @@ ZFP_HD PW lut_finish(unsigned& bits, unsigned& n, Reader& rd, bool& slow, unsign
           // count in chunk B (as implied_end for the first pair)
           const uint32_t q2 = q - npos;  // npos <= q while open
           io = pA > q2 ? parsed + st + q2 + (uint32_t)__builtin_popcount(oA & ((1u << q2) - 1u))
-                       : parsed + kChunkBits + (eA >> 31) + (q2 - pA) +
+                       : parsed + kChunkBits + ent_state(eA) + (q2 - pA) +
                              (uint32_t)__builtin_popcount(oB & ((1u << ((q2 - pA) & 31u)) - 1u));
           ones |= o << (npos & 63u);
-          npos += (T >> kPosShift) & 31u;
-          const uint32_t u = T & kUsedMask;
+          npos += ent_pos(T);
+          const uint32_t u = ent_used(T);
           ended = u >= kNotEnded;
           parsed += u & (kNotEnded - 1u);
-          st = eB >> 31;
+          st = ent_state(eB);
           open = !ended && parsed < b1 && nf + npos < N;
         }
       }
@@ -1638,7 +1650,7 @@ ZFP_HD PW lut_finish(unsigned& bits, unsigned& n, Reader& rd, bool& slow, unsign
       uint64_t o64 = ones;
       uint32_t o = implied_end(e1, e2, q, o64);
       // reached in a continuation pair: its count from the loop
-      if (((e1 >> kPosShift) & 31u) + ((e2 >> kPosShift) & 31u) <= q) o = io;
+      if (ent_pos(e1) + ent_pos(e2) <= q) o = io;
       // position N-1 within the budget: the code ends there; the budget
       // running out first leaves the cut result above (slow unless its one
       // lies at or below N-1)
@@ -1685,10 +1697,9 @@ ZFP_HD PW decode_plane_lut(unsigned& bits, unsigned& n, Reader& rd, bool& slow) 
     e1 = rd.chunk1_fast(g);
     e2 = 0;
   } else {
-    uint32_t e2a, e2b;
-    rd.chunks_fast(g, e1, e2a, e2b);
-    const uint32_t e2s = (e1 & kEntryState) ? e2b : e2a;
-    e2 = keep_if_bit13(e2s, e1);  // nothing after a chunk 1 that ended
+    uint32_t sel, e2a, e2b;
+    rd.chunks_fast(g, e1, sel, e2a, e2b);
+    e2 = perm_sel(e2b, e2a, sel);  // by chunk 1's exit state; nothing after a chunk 1 that ended
   }
   return lut_finish<DIMS, PW>(bits, n, rd, slow, nf, m, w, e1, e2);
 }
@@ -1736,11 +1747,11 @@ ZFP_HD PW decode_plane_fast_any(unsigned& n, Reader& rd) {
   // reads after the lookups' (Reader::window_g / window_w)
   WRaw wr;
   const uint32_t g = rd.window_g(nf, wr);
-  uint32_t e1, e2, e2a = 0, e2b = 0;
+  uint32_t e1, e2, sel = 0, e2a = 0, e2b = 0;
   if constexpr (DIMS == 1)
     e1 = rd.chunk1_fast(g);  // a 1D code fits chunk 1
   else
-    rd.chunks_fast(g, e1, e2a, e2b);
+    rd.chunks_fast(g, e1, sel, e2a, e2b);
   sched_fence();
   rd.lds_wait();  // one wait for the lookups (and the window's dwords)
   sched_fence();
@@ -1748,32 +1759,26 @@ ZFP_HD PW decode_plane_fast_any(unsigned& n, Reader& rd) {
   if constexpr (DIMS == 1) {
     e2 = 0;
   } else {
-    // the exit state (bit 31) as a mask by one arithmetic shift selects the
-    // chunk-2 entry, and bit 13 of chunk 1 (not ended) keeps it: plain
-    // expressions (an inline-asm result read by the next VALU instruction
-    // costs an s_nop), the mask laundered so that it stays a bit select
-    const uint32_t st = launder((uint32_t)((int32_t)e1 >> 31));
-    e2 = ((e2b & st) | (e2a & ~st)) & sbfe1(e1, 13);
+    // the chunk-2 entry by chunk 1's exit state, or none after a chunk 1 that
+    // ended: one v_perm_b32 by the selector stored beside chunk 1's entry
+    e2 = perm_sel(e2b, e2a, sel);
   }
   const uint32_t S = e1 + e2;
-  const uint32_t npos = S >> kPosShift & 31u;
-  const uint32_t used = S & kUsedMask;
+  const uint32_t nfp = nf + ent_pos(S);
   // One wave-uniform test for both rare cases: a code longer than the two
-  // chunks (the sum carries the marker) and one reaching position N-1
-  // (nf + npos >= N; nf + npos < 2N).
-  // (As one compare: used | (nf + npos) << (13 - 2 DIMS) reaches 2^13 exactly
-  // when used carries the marker or nf + npos >= N -- both parts are below
-  // 2^14, and below 2^13 otherwise.  One v_lshl_or_b32 with inline constants:
-  // a 0x2000 mask would need an SGPR reloaded every plane.)
-  const uint32_t nfp = nf + npos;
-  if (__builtin_expect(any_lane((used | (nfp << (13 - 2 * DIMS))) > rd.rare_lim), 0)) {
+  // chunks (the sum carries the marker: it is negative) and one reaching
+  // position N-1 (nf + npos >= N).  As one sign test: (nfp + 64 - N) << 25
+  // has its sign bit set exactly when nfp >= N (nfp + 64 - N < 128), and the
+  // OR with S keeps S's (bits 25-30 of both are don't-cares).
+  const int32_t rare = (int32_t)(S | ((nfp + (64u - N)) << 25));
+  if (__builtin_expect(any_lane(rare < 0), 0)) {
     // The budget-aware resolution from the entries already read
     // (lut_finish) for the whole wave, and for the lanes it cannot finish
     // (none on the bench fields: tools/dec_paths.cpp) the general decoder.
     // Everything rare stays in this one branch, so the common path carries
     // no flag from it.
     // (design statistics, tools/dec_paths.cpp: why a lane is rare)
-    ZFP_COUNT_PATH((S & kNotEnded) ? 16 : (nf + npos >= N) ? 17 : 18);
+    ZFP_COUNT_PATH((S & kMarkerBit) ? 16 : (nfp >= N) ? 17 : 18);
     const auto pos0 = rd.pos;
     unsigned bits = rd.end - rd.pos;
     bool slow;
@@ -1802,12 +1807,21 @@ ZFP_HD PW decode_plane_fast_any(unsigned& n, Reader& rd) {
   // of its verbatim part and a "0" leading test past its block: a
   // verbatim-only plane, all its bits.  So the common path only clips the
   // advance at the budget.
-  const uint32_t ones = ((e1 >> kOnesShift) & kChunkMask) |
-                        (((e2 >> kOnesShift) & kChunkMask) << ((e1 >> kPosShift) & 31u));
-  // bits >= nf of the plane from the group code, below it verbatim
-  const PW x = merge_at<PW>(nf, ones, w);
+  // (the ones: two ANDs with an inline constant and a v_lshl_or_b32 whose
+  // shift count is the low 5 bits of e1 >> 11, chunk 1's positions)
+  const uint32_t ones = ent_ones(e1) | (ent_ones(e2) << ((e1 >> kPosShift) & 31u));
+  PW x;
+  if constexpr (sizeof(PW) == 8) {
+    // bits >= nf of the plane from the group code, below it verbatim: w with
+    // its bits from nf on replaced by the ones, as w ^ (((w >> nf) ^ ones) <<
+    // nf) -- two 64-bit shifts and three XORs where the mask ~0 << nf, the
+    // shifted ones and two v_bfi_b32 took four slow-issue instructions
+    x = (PW)(w ^ (((w >> nf) ^ (uint64_t)ones) << nf));
+  } else {
+    x = merge_at<PW>(nf, ones, w);
+  }
   n = nfp;
-  rd.pos = umin(rd.pos + nf + used, rd.end);
+  rd.pos = umin(rd.pos + nf + ent_used(S), rd.end);
   return x;
 }
 
@@ -1929,7 +1943,6 @@ ZFP_HD void decode_planes(planes<UInt, DIMS>& P, unsigned budget, unsigned maxpr
   constexpr int PREC = (int)sizeof(UInt) * 8;
   unsigned n = 0;
   rd.end = rd.pos + budget;  // the reader never passes it
-  rd.rare_lim = uniform_const(kNotEnded - 1u);  // decode_plane_fast_any's rare test
   if constexpr (!(kLazyZero && DIMS == 3)) P.zero();
   if constexpr (PREC == 32) {
     // every plane down to 0 (see encode_planes); the early exits of the

@@ -56,7 +56,6 @@ struct HostReader {
   size_t words;
   size_t pos;
   size_t end;  // the block's last bit + 1: the stream reads as zeros from there (as on the GPU)
-  uint32_t rare_lim;  // (see LdsReader)
   uint64_t word(size_t i) const { return i < words ? s[i] : 0; }
   uint64_t peek() const {
     if (pos >= end) return 0;
@@ -99,11 +98,12 @@ struct HostReader {
     static const cuzfp::ChunkLut t = cuzfp::make_chunk_lut();
     return t;
   }
-  void chunks_fast(uint32_t g, uint32_t& e1, uint32_t& e2a, uint32_t& e2b) const {
+  void chunks_fast(uint32_t g, uint32_t& e1, uint32_t& sel, uint32_t& e2a, uint32_t& e2b) const {
     const uint32_t* t = table().e;
     const uint32_t gm = (g & 1u) ? g : 0u;
     const uint32_t c2 = gm >> cuzfp::kChunkBits;
     e1 = t[cuzfp::lut_s2_index(gm)];
+    sel = t[cuzfp::lut_s2_index(gm) + 1];
     e2a = t[cuzfp::lut_pair_index(c2, 0)];
     e2b = t[cuzfp::lut_pair_index(c2, 1)];
   }

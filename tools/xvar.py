@@ -1,6 +1,8 @@
 """Fast timing variants of the 3D float32 kernels (design tool, not the product).
 
   python tools/xvar.py build NAME "-DFLAG=1 ..." [NAME "FLAGS" ...]   # here
+    ("@f64": the double kernels; "@src=DIR": the kernels of another csrc tree,
+     e.g. an older commit's, `git archive REV cuzfp_amd/csrc | tar -x -C build/ab`)
   python tools/xvar.py isa NAME [NAME ...]                            # here: ISA histograms
   python tools/xvar.py run [--size S] [--field F] [--dims D --rate R] NAME [NAME ...]   # GPU box
     (variants built with -DCUZFP_XVAR_DIMS=D for 1D / 2D)
@@ -51,6 +53,14 @@ def _unit(flags: str) -> str:  # "@f64" in a variant's flags: the double kernels
     return "inst_f64" if "@f64" in flags.split() else "inst_f32"
 
 
+def _src(flags: str) -> str:  # "@src=DIR" in a variant's flags: kernels from another csrc tree (A/B)
+    from cuzfp_amd import build as b
+    for f in flags.split():
+        if f.startswith("@src="):
+            return os.path.join(ROOT, f[5:])
+    return b.CSRC
+
+
 def build(pairs):
     from cuzfp_amd import build as b
     procs = []
@@ -58,9 +68,9 @@ def build(pairs):
         d = os.path.join(OUT, name)
         os.makedirs(d, exist_ok=True)
         u = _unit(flags)
-        fl = [f for f in flags.split() if f != "@f64"]
+        fl = [f for f in flags.split() if not f.startswith("@")]
         procs.append(subprocess.Popen([b.HIPCC, *b.CXXFLAGS, "-DCUZFP_XVAR", *fl, "-c",
-                                       os.path.join(b.CSRC, u + ".hip"), "-o", os.path.join(d, "inst_f32.o")]))
+                                       os.path.join(_src(flags), u + ".hip"), "-o", os.path.join(d, "inst_f32.o")]))
     assert all(p.wait() == 0 for p in procs)
     for name, flags in pairs:
         d = os.path.join(OUT, name)
