@@ -209,6 +209,11 @@ template <int DIMS, typename UInt, int... I>
 ZFP_HD void permute_inv(const UInt* u, UInt* q, UInt nb, seq<I...>) {
   ((q[pidx<DIMS, I>::value] = from_negabinary(u[I], nb)), ...);
 }
+// the coefficients already finished (planes::store_hi<true>)
+template <int DIMS, typename UInt, int... I>
+ZFP_HD void permute_inv_copy(const UInt* u, UInt* q, seq<I...>) {
+  ((q[pidx<DIMS, I>::value] = u[I]), ...);
+}
 // the same for u already XOR-ed with nb (planes::store<true>): one subtraction
 template <int DIMS, typename UInt, int... I>
 ZFP_HD void permute_inv_sub(const UInt* u, UInt* q, UInt nb, seq<I...>) {
@@ -572,6 +577,57 @@ template <typename UInt, int DIMS> struct planes {
   }
 
   ZFP_HD void zero() { w.zero(); }
+
+  // 2D (16 coefficients of 32 bits), planes 16..31 only (round 6).  A 2D
+  // block's word r holds plane r in its low half and plane r + 16 in its high
+  // half, so the full transpose moves two 16 x 16 tiles at once; when only the
+  // high tile matters -- the encoder's first planes, the decoder of a wave
+  // whose lanes all stopped above plane 16 (BASELINE's 2D rate 2 stops above
+  // plane 20) -- the high tile alone is one 16 x 16 bit transpose in 8 dwords:
+  // dword k = row k | row k + 8 << 16, whose off-diagonal 8 x 8 blocks swap by
+  // the same byte permute that packs the rows, then three butterfly stages of
+  // 8 x 8 tiles.  8 v_perm_b32 and 36 stage instructions instead of 88.
+  //   load_hi: plane 16 + k (k < 8) in the high half of word k, plane 24 + k
+  //   in the high half of word k + 8 (get() of planes 16..31 reads these; the
+  //   low halves hold other bits until load() fills the block for planes
+  //   0..15).
+  template <bool NEG_ODD = false>
+  ZFP_HD void load_hi(const UInt* u) {
+    static_assert(DIMS == 2 && H == 1, "2D 32-bit blocks");
+    uint32_t d[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) d[k] = perm_bytes(u[k + 8], u[k], 0x07030602u);
+    transpose_tiles<8, NEG_ODD ? kOddWords : kInvNone>(d);
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      w.set(0, 0, k, d[k] << 16);
+      w.set(0, 0, k + 8, d[k]);
+    }
+  }
+  //   store_hi: the planes' low halves are zero (planes 0..15 unset); the
+  //   coefficients come out finished, q = (u ^ NB) - NB for NEG_ODD (the odd
+  //   bits inverted by the last stage, then the rest of the conversion on the
+  //   16-bit halves: two fast instructions a coefficient).
+  template <bool NEG_ODD = false>
+  ZFP_HD void store_hi(UInt* q) const {
+    static_assert(DIMS == 2 && H == 1, "2D 32-bit blocks");
+    uint32_t d[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) d[k] = perm_bytes(w.get(0, 0, k + 8), w.get(0, 0, k), 0x07030602u);
+    transpose_tiles<8, NEG_ODD ? kOddBits : kInvNone>(d);
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      if constexpr (NEG_ODD) {
+        // u ^ NB = (d << 16) | 0xaaaa, so (u ^ NB) - NB = (d - 0xaaaa) << 16; the
+        // high coefficient: (d & 0xffff0000) | 0xaaaa, less NB
+        q[k] = (d[k] - 0xaaaau) << 16;
+        q[k + 8] = (d[k] & 0xffff0000u) - 0xaaaa0000u;
+      } else {
+        q[k] = d[k] << 16;
+        q[k + 8] = d[k] & 0xffff0000u;
+      }
+    }
+  }
 
   // plane c (0..31) of half h as an N-bit word (bit i = that bit of
   // coefficient i); h is a compile-time constant, c may be a runtime value
@@ -1019,10 +1075,12 @@ ZFP_HD bool encode_half(const planes<UInt, DIMS>& P, unsigned& n, int cmin, Writ
 // register, so there is no VGPR-relative addressing (s_set_gpr_idx_on / off
 // around each read), no readfirstlane of the plane number, and the priority
 // drops sit at fixed trips.
-template <int H, int C, bool PRI = true, typename UInt, int DIMS, typename Writer>
+// (STOP: the lowest plane coded, STOP even; planes STOP-1 .. 0 are left to a
+// later call, as the 2D split of encode_block does)
+template <int H, int C, bool PRI = true, int STOP = 0, typename UInt, int DIMS, typename Writer>
 ZFP_HD bool encode_half_fixed(const planes<UInt, DIMS>& P, unsigned& n, Writer& wr) {
   typedef typename plane_word<DIMS>::type PW;
-  if constexpr (C >= 1) {
+  if constexpr (C >= STOP + 1) {
     if (!any_lane(!wr.full())) return false;
     wr.settle();
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(CUZFP_NO_PRIO)
@@ -1034,7 +1092,7 @@ ZFP_HD bool encode_half_fixed(const planes<UInt, DIMS>& P, unsigned& n, Writer& 
 #endif
     encode_plane_step<DIMS>((PW)P.template get<H>(C), n, wr);
     encode_plane_step<DIMS>((PW)P.template get<H>(C - 1), n, wr);
-    return encode_half_fixed<H, C - 2, PRI>(P, n, wr);
+    return encode_half_fixed<H, C - 2, PRI, STOP>(P, n, wr);
   }
   return true;
 }
@@ -1772,6 +1830,7 @@ ZFP_HD PW decode_plane_fast_any(unsigned& n, Reader& rd) {
   // OR with S keeps S's (bits 25-30 of both are don't-cares).
   const int32_t rare = (int32_t)(S | ((nfp + (64u - N)) << 25));
   if (__builtin_expect(any_lane(rare < 0), 0)) {
+    const auto pos0 = rd.pos;
     // The budget-aware resolution from the entries already read
     // (lut_finish) for the whole wave, and for the lanes it cannot finish
     // (none on the bench fields: tools/dec_paths.cpp) the general decoder.
@@ -1779,7 +1838,6 @@ ZFP_HD PW decode_plane_fast_any(unsigned& n, Reader& rd) {
     // no flag from it.
     // (design statistics, tools/dec_paths.cpp: why a lane is rare)
     ZFP_COUNT_PATH((S & kMarkerBit) ? 16 : (nfp >= N) ? 17 : 18);
-    const auto pos0 = rd.pos;
     unsigned bits = rd.end - rd.pos;
     bool slow;
     PW x = lut_finish<DIMS, PW>(bits, n, rd, slow, nf, umin(nf, bits), w, e1, e2);
@@ -1938,8 +1996,10 @@ ZFP_HD void decode_planes_1d(planes<UInt, 1>& P, uint32_t& n12, Reader& rd) {
   }
 }
 
+// Returns the highest plane left unset by a 32-bit coefficients' loop (-1:
+// none; every plane below it is unset too), 31 otherwise (nothing known).
 template <typename UInt, int DIMS, typename Reader>
-ZFP_HD void decode_planes(planes<UInt, DIMS>& P, unsigned budget, unsigned maxprec, Reader& rd) {
+ZFP_HD int decode_planes(planes<UInt, DIMS>& P, unsigned budget, unsigned maxprec, Reader& rd) {
   constexpr int PREC = (int)sizeof(UInt) * 8;
   unsigned n = 0;
   rd.end = rd.pos + budget;  // the reader never passes it
@@ -1951,9 +2011,9 @@ ZFP_HD void decode_planes(planes<UInt, DIMS>& P, unsigned budget, unsigned maxpr
     if constexpr (DIMS == 1 && has_dec1d<Reader>::value) {
       uint32_t n12 = 0;
       decode_planes_1d<0, 31>(P, n12, rd);
-      return;
+      return 31;
     }
-    decode_half_fixed<0, 31>(P, n, rd);
+    return decode_half_fixed<0, 31>(P, n, rd);
   } else {
     const int kmin = PREC > (int)maxprec ? PREC - (int)maxprec : 0;
     if constexpr (DIMS == 1 && has_dec1d<Reader>::value) {
@@ -1961,7 +2021,7 @@ ZFP_HD void decode_planes(planes<UInt, DIMS>& P, unsigned budget, unsigned maxpr
         uint32_t n12 = 0;
         decode_planes_1d<1, 31>(P, n12, rd);
         decode_planes_1d<0, 31>(P, n12, rd);
-        return;
+        return 31;
       }
     }
     // (64-bit values keep the rolled loop: unrolled, the f64 decoder measured
@@ -1969,10 +2029,11 @@ ZFP_HD void decode_planes(planes<UInt, DIMS>& P, unsigned budget, unsigned maxpr
     zero_planes<1>(P, decode_half<1>(P, n, kmin > 32 ? kmin - 32 : 0, rd));
     if (kmin >= 32) {
       zero_planes<0>(P, 31);
-      return;
+      return 31;
     }
     zero_planes<0>(P, decode_half<0>(P, n, kmin, rd));
   }
+  return 31;
 }
 
 // ---------------------------------------------------------------------------
@@ -2212,9 +2273,24 @@ ZFP_HD void encode_block(const Scalar* f, unsigned maxbits, Writer& wr) {
   (void)maxprec;
 #else
   planes<UInt, DIMS> P;
-  P.template load<true>(u);
-  ZFP_STAMP(3);
-  encode_planes<UInt, DIMS>(P, maxprec, wr);
+  if constexpr (DIMS == 2 && sizeof(UInt) == 4) {
+    // 2D 32-bit blocks: planes 31..16 from the high tile alone (load_hi),
+    // the low tile only if some lane of the wave still has budget after
+    // plane 16 (never at BASELINE's 2D rate 2, whose blocks stop above plane
+    // 20).  (precision() is 32 here: every plane down to 0, as encode_planes.)
+    P.template load_hi<true>(u);
+    ZFP_STAMP(3);
+    (void)maxprec;
+    unsigned n = 0;
+    if (encode_half_fixed<0, 31, true, 16>(P, n, wr)) {
+      P.template load<true>(u);
+      encode_half_fixed<0, 15>(P, n, wr);
+    }
+  } else {
+    P.template load<true>(u);
+    ZFP_STAMP(3);
+    encode_planes<UInt, DIMS>(P, maxprec, wr);
+  }
   ZFP_STAMP(4);
 #endif
   wr.finish();
@@ -2274,20 +2350,35 @@ ZFP_HD bool decode_block(Scalar* f, unsigned maxbits, Reader& rd) {
   P.store(u);
 #else
   planes<UInt, DIMS> P;
-  decode_planes<UInt, DIMS>(P, budget, maxprec, rd);
+  const int unset = decode_planes<UInt, DIMS>(P, budget, maxprec, rd);
+  (void)unset;
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(CUZFP_NO_PRIO) && CUZFP_DPRIO_AFTER >= 0
   if constexpr (prio_of<Reader>::value) __builtin_amdgcn_s_setprio(CUZFP_DPRIO_AFTER);  // see progress_priority
 #endif
   ZFP_STAMP(1);
-  P.template store<true>(u);  // u ^ NB
-  ZFP_STAMP(2);
-#endif
   UInt q[N];
   constexpr UInt NB = nbmask<UInt>::value;
+  if constexpr (DIMS == 2 && sizeof(UInt) == 4) {
+    // planes 15..0 unset on every lane of the wave (a wave-uniform loop
+    // exit): the high tile alone, coefficients finished by store_hi
+    if (unset >= 15) {
+      P.template store_hi<true>(u);  // (u ^ NB) - NB
+      permute_inv_copy<DIMS>(u, q, make_seq<N>());
+    } else {
+      P.template store<true>(u);  // u ^ NB
+      permute_inv_sub<DIMS>(u, q, NB, make_seq<N>());  // (u ^ NB) - NB
+    }
+    ZFP_STAMP(2);
+  } else {
+    P.template store<true>(u);  // u ^ NB
+    ZFP_STAMP(2);
+    permute_inv_sub<DIMS>(u, q, NB, make_seq<N>());  // (u ^ NB) - NB
+  }
+#endif
 #if defined(CUZFP_PROBE) && (CUZFP_PROBE == 1 || CUZFP_PROBE == 2)
+  UInt q[N];
+  constexpr UInt NB = nbmask<UInt>::value;
   permute_inv<DIMS>(u, q, NB, make_seq<N>());
-#else
-  permute_inv_sub<DIMS>(u, q, NB, make_seq<N>());  // (u ^ NB) - NB
 #endif
   inv_xform<DIMS>(q);
   ZFP_STAMP(3);
