@@ -1828,7 +1828,9 @@ ZFP_HD PW decode_plane_fast_any(unsigned& n, Reader& rd) {
   // position N-1 (nf + npos >= N).  As one sign test: (nfp + 64 - N) << 25
   // has its sign bit set exactly when nfp >= N (nfp + 64 - N < 128), and the
   // OR with S keeps S's (bits 25-30 of both are don't-cares).
-  const int32_t rare = (int32_t)(S | ((nfp + (64u - N)) << 25));
+  // (the biased count laundered: the compiler otherwise distributes the shift,
+  // (nfp << 25) + (64 - N) << 25, and re-materialises that constant every step)
+  const int32_t rare = (int32_t)(S | ((N == 64 ? nfp : launder(nfp + (64u - N))) << 25));
   if (__builtin_expect(any_lane(rare < 0), 0)) {
     const auto pos0 = rd.pos;
     // The budget-aware resolution from the entries already read

@@ -1,11 +1,11 @@
 #!/bin/bash
-# tools/r05_session.sh TAG STEPS... -- one GPU-box session of round 5's work:
+# tools/session.sh TAG STEPS... -- one GPU-box session:
 # xvar A/B timing of kernel variants, the launch-overhead probe, GPU tests,
 # bench, rocprofv3 stats / counters.  Every GPU step runs under its own time
 # limit; a crash / abort / timeout ends the session at once (pytest's exit 1,
 # "tests failed", is reported and also ends it).
 set -u
-TAG=${1:-r05}
+TAG=${1:-r06}
 shift || true
 OUT=${GRAFT_REPO_ROOT:-$PWD}/gpurun_out
 mkdir -p "$OUT"
