@@ -64,6 +64,10 @@ namespace cuzfp {
 // each decode workgroup copies them to LDS.
 __device__ const ChunkLut g_chunk_lut = make_chunk_lut();
 constexpr size_t kChunkLutBytes = sizeof(ChunkLut);
+// the part a DIMS-dimensional decoder holds in LDS: 1D reads chunk 1's table
+// alone (a 1D group code fits one chunk), 8 of the 16 KiB
+template <int DIMS>
+constexpr size_t chunk_lut_bytes() { return DIMS == 1 ? kLutPairs * 4 : kChunkLutBytes; }
 // ... and the plane coder's spread tables (2 KiB): a static LDS array at
 // address 0, so a lookup is one ds_read_b32 at (byte << 2) with the table in
 // the offset field.  Every wave of a workgroup writes the whole table itself
@@ -816,8 +820,11 @@ __device__ __forceinline__ void scatter_f64_staged(double* __restrict__ data, co
 #ifndef CUZFP_F64_ENC_WAVES
 #define CUZFP_F64_ENC_WAVES 2
 #endif
+#ifndef CUZFP_F64_DEC_WAVES  // A/B builds
+#define CUZFP_F64_DEC_WAVES 2
+#endif
 template <typename Scalar, int DIMS, bool ENC = false> struct occupancy {
-  static constexpr int value = (sizeof(Scalar) == 8 && DIMS == 3) ? (ENC ? CUZFP_F64_ENC_WAVES : 2) : 4;
+  static constexpr int value = (sizeof(Scalar) == 8 && DIMS == 3) ? (ENC ? CUZFP_F64_ENC_WAVES : CUZFP_F64_DEC_WAVES) : 4;
 };
 
 // REG (1D/2D, maxbits 32 or 64): the block is coded into a register
@@ -926,6 +933,18 @@ __device__ __forceinline__ void zfp_encode_body(const Scalar* __restrict__ data,
   if constexpr (ALIGNED) {
     uint64_t* mine = lds + lane;
     for (uint32_t j = 0; j < W + kSlackWords; j++) mine[j * 64] = 0;  // own column
+    // The workgroup's waves (one on each SIMD of the CU) start coding
+    // together, once every one of their blocks has landed: 256^3 r8 step
+    // 46.04 / 45.80 -> 45.57 / 45.54 us (polynomial), 44.58 / 44.71 ->
+    // 44.46 / 44.60 (splitmix), profiles/r06_ab_ebar.txt; the decoder's
+    // barrier over its stream segments does the same (taking it away measured
+    // +2 us, r06_ab_copyin.txt).  Only where every wave of the workgroup is
+    // live (a wave-uniform test, the same on all of them): the others
+    // returned above.
+    if (g.wave0 + (bid + 1) * (blockDim.x >> 6) <= g.wave_end) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
     wave_lds_sync();  // the tables
     LdsOrWriter<PRIO> wr{mine, lut, 0, 64 * W, p1d, uniform_const64(0x7fffu)};
     encode_block<Scalar, DIMS>(f, g.maxbits, wr);
@@ -1223,7 +1242,7 @@ template <typename Scalar, int DIMS, bool FAST, bool PRIO = true, int REG = 0, i
 __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) void zfp_decode(const uint64_t* __restrict__ stream,
                                                                       Geometry g,
                                                                       Scalar* __restrict__ data) {
-  __shared__ __attribute__((aligned(16))) uint32_t ctab[kChunkLutBytes / 4];  // LDS address 0 (static)
+  __shared__ __attribute__((aligned(16))) uint32_t ctab[chunk_lut_bytes<DIMS>() / 4];  // LDS address 0 (static)
   // 1D: the plane table (Plane1dDecLut, 16 KiB)
   __shared__ __attribute__((aligned(16))) uint16_t dtab[DIMS == 1 ? sizeof(Plane1dDecLut) / 2 : 8];
   zfp_decode_body<Scalar, DIMS, FAST, PRIO, REG, WPG>(stream, g, data, blockIdx.x, ctab, dtab);
@@ -1312,7 +1331,7 @@ __global__ __launch_bounds__(kLanes * WPG, (occupancy<Scalar, DIMS>::value)) voi
     const uint64_t* __restrict__ stream, Geometry g, Scalar* __restrict__ data) {
   static_assert(DIMS <= 2 && K >= 2 && K <= 8, "register-reader batches: 1D/2D, 2-8 a wave");
   constexpr int N = 1 << (2 * DIMS);
-  __shared__ __attribute__((aligned(16))) uint32_t ctab[kChunkLutBytes / 4];  // LDS address 0 (static)
+  __shared__ __attribute__((aligned(16))) uint32_t ctab[chunk_lut_bytes<DIMS>() / 4];  // LDS address 0 (static)
   __shared__ __attribute__((aligned(16))) uint16_t dtab[DIMS == 1 ? sizeof(Plane1dDecLut) / 2 : 8];
   const uint32_t wig = wave_in_group();
   const uint32_t lane = threadIdx.x & 63;
@@ -1528,7 +1547,7 @@ int launch_decode_t(const uint64_t* stream, const Geometry& g, bool fast, void* 
   // blocks of at most 64 bits are read into registers (RegReader): no LDS image
   const bool reg = DIMS <= 2 && g.maxbits <= 64;
   if (reg) gg.lds_words = 0;
-  const size_t kStatic = kChunkLutBytes + (DIMS == 1 ? sizeof(Plane1dDecLut) : 16);
+  const size_t kStatic = chunk_lut_bytes<DIMS>() + (DIMS == 1 ? sizeof(Plane1dDecLut) : 16);
   // one wave's image beside the tables must fit the workgroup's LDS budget
   if (gg.lds_words * 8 + kStatic > lds_cap_bytes()) return CUZFP_ERROR_INVALID_ARGUMENT;
   const uint32_t wpg = waves_per_group(gg.lds_words, kStatic, kDecWaves);
