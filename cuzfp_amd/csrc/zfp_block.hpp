@@ -411,7 +411,7 @@ ZFP_HD void shr2(uint32_t& x, uint32_t& y, uint32_t sj) {
 }
 
 template <int J, int INV = kInvNone>
-ZFP_HD void transpose_stage(uint32_t* a, int rows) {
+ZFP_HD void transpose_stage(uint32_t* a, int rows, int r0 = 0) {  // rows r0 .. rows-1 (J < 16: a closed set)
   // swap the J x J off-diagonal sub-blocks of every 2J x 2J tile:
   //   lo' = (lo & m) | ((hi << J) & ~m),  hi' = ((lo >> J) & m) | (hi & ~m)
   // one v_perm_b32 per word for the byte-granular stages; the bit-granular
@@ -426,7 +426,7 @@ ZFP_HD void transpose_stage(uint32_t* a, int rows) {
     const uint32_t sj = opaque_shift<J>();
 #pragma unroll
     for (int i = 0; i < 32; i++) {
-      if (i >= rows || (i & J) || (i & D)) continue;
+      if (i < r0 || i >= rows || (i & J) || (i & D)) continue;
       const int i2 = i + D;
       uint32_t h1 = a[i + J], h2 = a[i2 + J], l1 = a[i], l2 = a[i2];
       const uint32_t H1 = h1, H2 = h2;  // hi words as they were
@@ -448,7 +448,7 @@ ZFP_HD void transpose_stage(uint32_t* a, int rows) {
   }
 #pragma unroll
   for (int i = 0; i < 32; i++) {
-    if (i >= rows || (i & J)) continue;
+    if (i < r0 || i >= rows || (i & J)) continue;
     const uint32_t lo = a[i], hi = a[i + J];
     if constexpr (J == 16) {
       a[i] = perm_bytes(hi, lo, 0x05040100u);
@@ -524,12 +524,14 @@ template <int H, int G, int R> struct plane_words<H, G, R, true> {
 // coefficients W = N words; 64-bit coefficients are split into low and high
 // halves (planes 0..31 from the low words, 32..63 from the high words).
 // Word (h, g, row) = word g*R + row of half h.
-template <typename UInt, int DIMS> struct planes {
+// VEC: tuple storage (the rolled loops' runtime plane numbers); plain
+// registers otherwise
+template <typename UInt, int DIMS, bool VEC = (sizeof(UInt) == 8)> struct planes {
   static constexpr int N = 1 << (2 * DIMS);
   static constexpr int H = sizeof(UInt) / 4;      // 32-bit halves per value
   static constexpr int R = N < 32 ? N : 32;       // tile height
   static constexpr int G = N / R;                 // row groups (2 for 3D)
-  plane_words<H, G, R, (H == 2)> w;
+  plane_words<H, G, R, VEC> w;
 
   // NEG_ODD: u holds q + 0xaaaa... and the planes get the negabinary's
   // final "^ 0xaaaa..." (the odd planes inverted) from the transpose
@@ -577,6 +579,91 @@ template <typename UInt, int DIMS> struct planes {
   }
 
   ZFP_HD void zero() { w.zero(); }
+
+  // 3D 64-bit blocks in three steps (round 6): BASELINE's 3D f64 rate 16
+  // codes planes 63..~21, so the low half's planes 15..0 are rarely reached.
+  //   load_split: the high half's tiles transposed (planes 63..32), the low
+  //   half's through the J = 16 stage (it moves bits between the row halves;
+  //   the stages commute, so it may go first);
+  //   lo_part<UPPER>: the low half's J = 8..1 stages on rows 16..31 (planes
+  //   31..16; their pairs stay within a 16-row half), lo_part<!UPPER> on rows
+  //   0..15 (planes 15..0).
+  // Together the same words as load(): 88 slow instructions a tile are left
+  // out when no lane of the wave reaches plane 15.
+  template <bool NEG_ODD = false>
+  ZFP_HD void load_split(const UInt* u) {
+    static_assert(H == 2 && N == 64, "3D 64-bit blocks");
+    uint32_t t[H][N];
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      t[0][i] = (uint32_t)u[i];
+      t[1][i] = (uint32_t)((uint64_t)u[i] >> 32);
+    }
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+      transpose_tiles<R, NEG_ODD ? kOddWords : kInvNone>(&t[1][g * R]);
+      transpose_stage<16>(&t[0][g * R], R);
+    }
+#pragma unroll
+    for (int h = 0; h < H; h++)
+#pragma unroll
+      for (int g = 0; g < G; g++)
+#pragma unroll
+        for (int r = 0; r < R; r++) w.set(h, g, r, t[h][g * R + r]);
+  }
+  template <bool NEG_ODD = false, bool UPPER = true>
+  ZFP_HD void lo_part() {
+    constexpr int INV = NEG_ODD ? kOddWords : kInvNone;
+    constexpr int r0 = UPPER ? 16 : 0, r1 = UPPER ? 32 : 16;
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+      uint32_t t[R];
+#pragma unroll
+      for (int r = r0; r < r1; r++) t[r] = w.get(0, g, r);
+      transpose_stage<8>(t, r1, r0);
+      transpose_stage<4>(t, r1, r0);
+      transpose_stage<2>(t, r1, r0);
+      transpose_stage<1, INV>(t, r1, r0);
+#pragma unroll
+      for (int r = r0; r < r1; r++) w.set(0, g, r, t[r]);
+    }
+  }
+
+  //   store_split: store() for a block whose planes 15..0 are zero on every
+  //   lane: the low half's J = 8..1 stages on rows 16..31 only (rows 0..15
+  //   stay zero -- 0xaaaa... once the last stage inverts their odd bits for
+  //   NEG_ODD), then the J = 16 stage, whose low rows are those constants.
+  template <bool NEG_ODD = false>
+  ZFP_HD void store_split(UInt* u) const {
+    static_assert(H == 2 && N == 64, "3D 64-bit blocks");
+    constexpr int INV = NEG_ODD ? kOddBits : kInvNone;
+    constexpr uint32_t Z = NEG_ODD ? 0xaaaaaaaau : 0u;  // rows 0..15 after the J = 1 stage
+    uint32_t t[H][N];
+#pragma unroll
+    for (int g = 0; g < G; g++)
+#pragma unroll
+      for (int r = 0; r < R; r++) t[1][g * R + r] = w.get(1, g, r);
+#pragma unroll
+    for (int g = 0; g < G; g++) transpose_tiles<R, INV>(&t[1][g * R]);
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+      uint32_t* a = &t[0][g * R];
+#pragma unroll
+      for (int r = 16; r < R; r++) a[r] = w.get(0, g, r);
+      transpose_stage<8>(a, 32, 16);
+      transpose_stage<4>(a, 32, 16);
+      transpose_stage<2>(a, 32, 16);
+      transpose_stage<1, INV>(a, 32, 16);
+#pragma unroll
+      for (int i = 0; i < 16; i++) {
+        const uint32_t hi = a[i + 16];
+        a[i] = perm_bytes(hi, Z, 0x05040100u);
+        a[i + 16] = perm_bytes(hi, Z, 0x07060302u);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < N; i++) u[i] = (UInt)((uint64_t)t[0][i] | ((uint64_t)t[1][i] << 32));
+  }
 
   // 2D (16 coefficients of 32 bits), planes 16..31 only (round 6).  A 2D
   // block's word r holds plane r in its low half and plane r + 16 in its high
@@ -1077,8 +1164,8 @@ ZFP_HD bool encode_half(const planes<UInt, DIMS>& P, unsigned& n, int cmin, Writ
 // drops sit at fixed trips.
 // (STOP: the lowest plane coded, STOP even; planes STOP-1 .. 0 are left to a
 // later call, as the 2D split of encode_block does)
-template <int H, int C, bool PRI = true, int STOP = 0, typename UInt, int DIMS, typename Writer>
-ZFP_HD bool encode_half_fixed(const planes<UInt, DIMS>& P, unsigned& n, Writer& wr) {
+template <int H, int C, bool PRI = true, int STOP = 0, typename UInt, int DIMS, bool VEC, typename Writer>
+ZFP_HD bool encode_half_fixed(const planes<UInt, DIMS, VEC>& P, unsigned& n, Writer& wr) {
   typedef typename plane_word<DIMS>::type PW;
   if constexpr (C >= STOP + 1) {
     if (!any_lane(!wr.full())) return false;
@@ -1922,6 +2009,14 @@ ZFP_HD int decode_half(planes<UInt, DIMS>& P, unsigned& n, int cmin, Reader& rd)
 // into the layout its indexed moves use).  1D/2D planes share registers and
 // set() ORs, so that array is zeroed up front.  (CUZFP_EAGER_ZERO: zero up
 // front in 3D too.)
+// 3D 64-bit blocks: the low half's planes transposed in two parts, bit 0 the
+// encoder (planes::load_split), bit 1 the decoder (planes::store_split)
+#ifndef CUZFP_F64_SPLIT
+#define CUZFP_F64_SPLIT 0
+#endif
+#ifndef CUZFP_F64_SPLIT_VEC
+#define CUZFP_F64_SPLIT_VEC true
+#endif
 #ifndef CUZFP_EAGER_ZERO
 constexpr bool kLazyZero = true;
 #else
@@ -1998,8 +2093,9 @@ ZFP_HD void decode_planes_1d(planes<UInt, 1>& P, uint32_t& n12, Reader& rd) {
   }
 }
 
-// Returns the highest plane left unset by a 32-bit coefficients' loop (-1:
-// none; every plane below it is unset too), 31 otherwise (nothing known).
+// Returns the highest plane left unset by a 32-bit coefficients' loop, or by
+// the low half's loop of 64-bit ones (-1: none; every plane below it is unset
+// too), 31 where nothing is known.
 template <typename UInt, int DIMS, typename Reader>
 ZFP_HD int decode_planes(planes<UInt, DIMS>& P, unsigned budget, unsigned maxprec, Reader& rd) {
   constexpr int PREC = (int)sizeof(UInt) * 8;
@@ -2033,7 +2129,10 @@ ZFP_HD int decode_planes(planes<UInt, DIMS>& P, unsigned budget, unsigned maxpre
       zero_planes<0>(P, 31);
       return 31;
     }
-    zero_planes<0>(P, decode_half<0>(P, n, kmin, rd));
+    // the low half's highest unset plane (3D: planes::store_split)
+    const int c = decode_half<0>(P, n, kmin, rd);
+    zero_planes<0>(P, c);
+    return c;
   }
   return 31;
 }
@@ -2288,6 +2387,41 @@ ZFP_HD void encode_block(const Scalar* f, unsigned maxbits, Writer& wr) {
       P.template load<true>(u);
       encode_half_fixed<0, 15>(P, n, wr);
     }
+  } else if constexpr ((CUZFP_F64_SPLIT & 1) && DIMS == 3 && sizeof(UInt) == 8) {
+    // 3D 64-bit blocks: the low half's tiles transposed a 16-plane part at a
+    // time, each only if some lane of the wave still has budget
+    // (planes::load_split).  One consumer of u, in plain registers: a second
+    // layout of u for the rolled loops' tuples made the kernel spill.
+    planes<UInt, DIMS, CUZFP_F64_SPLIT_VEC> PS;
+    PS.template load_split<true>(u);
+    ZFP_STAMP(3);
+    unsigned n = 0;
+    if (__builtin_expect(!any_lane(maxprec != T::prec), 1)) {  // normal doubles, int64: down to plane 0
+      if (encode_half_fixed<1, 31>(PS, n, wr)) {
+        PS.template lo_part<true, true>();
+        if (encode_half_fixed<0, 31, false, 16>(PS, n, wr)) {
+          PS.template lo_part<true, false>();
+          encode_half_fixed<0, 15, false>(PS, n, wr);
+        }
+      }
+    } else {  // some lane stops above plane 0: encode_planes' rolled loops
+#ifndef CUZFP_TMP_NOELSE
+      PS.template lo_part<true, true>();
+      PS.template lo_part<true, false>();
+      const int kmin = 64 - (int)maxprec;
+      if constexpr (CUZFP_F64_SPLIT_VEC) {
+        if (encode_half<1>(PS, n, kmin > 32 ? kmin - 32 : 0, wr)) encode_half<0>(PS, n, kmin, wr);
+      } else {
+#pragma unroll
+        for (int h = 0; h < 2; h++)
+#pragma unroll
+          for (int g = 0; g < 2; g++)
+#pragma unroll
+            for (int r = 0; r < 32; r++) P.w.set(h, g, r, PS.w.get(h, g, r));
+        if (encode_half<1>(P, n, kmin > 32 ? kmin - 32 : 0, wr)) encode_half<0>(P, n, kmin, wr);
+      }
+#endif
+    }
   } else {
     P.template load<true>(u);
     ZFP_STAMP(3);
@@ -2371,6 +2505,15 @@ ZFP_HD bool decode_block(Scalar* f, unsigned maxbits, Reader& rd) {
       permute_inv_sub<DIMS>(u, q, NB, make_seq<N>());  // (u ^ NB) - NB
     }
     ZFP_STAMP(2);
+  } else if constexpr ((CUZFP_F64_SPLIT & 2) && DIMS == 3 && sizeof(UInt) == 8) {
+    // planes 15..0 unset on every lane of the wave (BASELINE's 3D f64 rate 16
+    // stops above plane 20): the low half's tiles from rows 16..31 alone
+    if (unset >= 15)
+      P.template store_split<true>(u);  // u ^ NB
+    else
+      P.template store<true>(u);
+    ZFP_STAMP(2);
+    permute_inv_sub<DIMS>(u, q, NB, make_seq<N>());  // (u ^ NB) - NB
   } else {
     P.template store<true>(u);  // u ^ NB
     ZFP_STAMP(2);

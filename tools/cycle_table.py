@@ -1,7 +1,7 @@
 """Issue-cycle table of the 3D float32 kernels: where a block's cycles go (design tool).
 
     python tools/cycle_table.py [--obj build/obj/inst_f32.o] [--ctr profiles/r06_counters.txt]
-                                [--stamps profiles/r06_stamps.txt] [--enc-us E --dec-us D]
+                                [--enc-us E --dec-us D]
 
 For each of the headline kernels (zfp_encode / zfp_decode<float, 3, FAST, PRIO>)
 the main path's ISA is cut into sections -- encoder: prologue (gathers,
@@ -106,7 +106,8 @@ def table(ks):
             t0 = first(lines, sgpr_perm)
             t1 = first(lines, lambda l: l.startswith("ds_read_b32"), t0)
             # a plane step: from one pair of ds_or_b64 (the put) to the next
-            puts = [i for i in range(t1, len(lines)) if lines[i].startswith("ds_or_b64") and
+            e = first(lines, lambda l: l.startswith("s_endpgm"), t1)  # in-line steps only (wide steps are laid out after it)
+            puts = [i for i in range(t1, e) if lines[i].startswith("ds_or_b64") and
                     i + 1 < len(lines) and lines[i + 1].startswith("ds_or_b64")]
             steps = [lines[i + 2:j + 2] for i, j in zip(puts, puts[1:]) if j - i < 80]
             st = sorted(steps, key=len)[len(steps) // 2] if steps else []
@@ -130,13 +131,31 @@ def table(ks):
     return rows
 
 
+def counters(path: str) -> dict:
+    """SQ_INSTS_VALU / SQ_WAVES of the 3D f32 kernels in a tools/counters.py report"""
+    out, kind, vals = {}, None, {}
+    for line in open(path):
+        m = re.match(r"^zfp_(encode|decode)<float, 3, true, true", line)
+        if m:
+            kind, vals = m.group(1), {}
+            continue
+        m = re.match(r"^\s+(SQ_\w+)\s+([0-9.e+]+)", line)
+        if kind and m:
+            vals[m.group(1)] = float(m.group(2))
+            if "SQ_INSTS_VALU" in vals and "SQ_WAVES" in vals:
+                out[kind] = vals["SQ_INSTS_VALU"] / vals["SQ_WAVES"]
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--obj", default=os.path.join(ROOT, "build", "obj", "inst_f32.o"))
     ap.add_argument("--enc-us", type=float, default=None, help="measured encode time (us) for the wall column")
     ap.add_argument("--dec-us", type=float, default=None)
+    ap.add_argument("--ctr", default=None, help="tools/counters.py output: dynamic VALU a wave beside the static count")
     a = ap.parse_args()
     rows = table(kernels(disassemble(a.obj)))
+    dyn = counters(a.ctr) if a.ctr else {}
     budget = BUDGET_US * 1e-6 * CLOCK_GHZ * 1e9 / BLOCKS_PER_SIMD
     print(f"issue cost: fast {C_FAST} / slow {C_SLOW} cycles a wave-instruction (4 waves a SIMD); "
           f"SIMD cycles a block = wave cycles / 64; clock {CLOCK_GHZ} GHz")
@@ -155,6 +174,9 @@ def main():
         extra = (DEC_RARE if kind == "decode" else ENC_WIDE)
         print(f"{'(not priced: ' + ('rare-path steps' if kind == 'decode' else 'wide steps') + f', ~{extra} a wave)':66s}")
         print(f"{'total, priced':66s} {tot[0]:7.0f} {tot[1]:7.0f} {tot[2]:7.0f} {tot[3]:9.0f} {tot[4]:9.1f}")
+        if kind in dyn:
+            v = dyn[kind]
+            print(f"{'dynamic (SQ counters): VALU a wave, SQ_INSTS_VALU / SQ_WAVES':66s} {v:7.0f}")
         us = a.enc_us if kind == "encode" else a.dec_us
         if us:
             wall = us * 1e-6 * CLOCK_GHZ * 1e9 / BLOCKS_PER_SIMD
