@@ -524,14 +524,12 @@ template <int H, int G, int R> struct plane_words<H, G, R, true> {
 // coefficients W = N words; 64-bit coefficients are split into low and high
 // halves (planes 0..31 from the low words, 32..63 from the high words).
 // Word (h, g, row) = word g*R + row of half h.
-// VEC: tuple storage (the rolled loops' runtime plane numbers); plain
-// registers otherwise
-template <typename UInt, int DIMS, bool VEC = (sizeof(UInt) == 8)> struct planes {
+template <typename UInt, int DIMS> struct planes {
   static constexpr int N = 1 << (2 * DIMS);
   static constexpr int H = sizeof(UInt) / 4;      // 32-bit halves per value
   static constexpr int R = N < 32 ? N : 32;       // tile height
   static constexpr int G = N / R;                 // row groups (2 for 3D)
-  plane_words<H, G, R, VEC> w;
+  plane_words<H, G, R, (H == 2)> w;
 
   // NEG_ODD: u holds q + 0xaaaa... and the planes get the negabinary's
   // final "^ 0xaaaa..." (the odd planes inverted) from the transpose
@@ -627,42 +625,6 @@ template <typename UInt, int DIMS, bool VEC = (sizeof(UInt) == 8)> struct planes
 #pragma unroll
       for (int r = r0; r < r1; r++) w.set(0, g, r, t[r]);
     }
-  }
-
-  //   store_split: store() for a block whose planes 15..0 are zero on every
-  //   lane: the low half's J = 8..1 stages on rows 16..31 only (rows 0..15
-  //   stay zero -- 0xaaaa... once the last stage inverts their odd bits for
-  //   NEG_ODD), then the J = 16 stage, whose low rows are those constants.
-  template <bool NEG_ODD = false>
-  ZFP_HD void store_split(UInt* u) const {
-    static_assert(H == 2 && N == 64, "3D 64-bit blocks");
-    constexpr int INV = NEG_ODD ? kOddBits : kInvNone;
-    constexpr uint32_t Z = NEG_ODD ? 0xaaaaaaaau : 0u;  // rows 0..15 after the J = 1 stage
-    uint32_t t[H][N];
-#pragma unroll
-    for (int g = 0; g < G; g++)
-#pragma unroll
-      for (int r = 0; r < R; r++) t[1][g * R + r] = w.get(1, g, r);
-#pragma unroll
-    for (int g = 0; g < G; g++) transpose_tiles<R, INV>(&t[1][g * R]);
-#pragma unroll
-    for (int g = 0; g < G; g++) {
-      uint32_t* a = &t[0][g * R];
-#pragma unroll
-      for (int r = 16; r < R; r++) a[r] = w.get(0, g, r);
-      transpose_stage<8>(a, 32, 16);
-      transpose_stage<4>(a, 32, 16);
-      transpose_stage<2>(a, 32, 16);
-      transpose_stage<1, INV>(a, 32, 16);
-#pragma unroll
-      for (int i = 0; i < 16; i++) {
-        const uint32_t hi = a[i + 16];
-        a[i] = perm_bytes(hi, Z, 0x05040100u);
-        a[i + 16] = perm_bytes(hi, Z, 0x07060302u);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < N; i++) u[i] = (UInt)((uint64_t)t[0][i] | ((uint64_t)t[1][i] << 32));
   }
 
   // 2D (16 coefficients of 32 bits), planes 16..31 only (round 6).  A 2D
@@ -835,6 +797,20 @@ ZFP_HD bool any_lane(bool p) {
 #define CUZFP_DPRIO_T0 (-1)
 #define CUZFP_DPRIO_AFTER 2
 #endif
+// the LDS reader's pipelined windows (LdsReader::prefetch_at): 1 every fast
+// step issues the next one's reads, 2 the first step of each pair only
+#ifndef CUZFP_DPIPE
+#define CUZFP_DPIPE 0
+#endif
+constexpr bool kPipeAll = CUZFP_DPIPE == 1;
+// Readers with pipelined windows: prefetch_at(p, m) issues the reads of the
+// windows at p + m and p, window_g_pipe(wr) takes them (kPipe)
+template <typename T, typename = void> struct pipe_of {
+  static constexpr bool value = false;
+};
+template <typename T> struct pipe_of<T, decltype((void)T::kPipe)> {
+  static constexpr bool value = T::kPipe;
+};
 // The schedule pays off when the launch is one resident round of waves (256^3
 // f32: 4 waves per SIMD, all resident at once).  Over several rounds it costs
 // 12 % (1024^3: step 3.63 -> 3.19 ms without it; tools/variants.py): a wave
@@ -1164,8 +1140,8 @@ ZFP_HD bool encode_half(const planes<UInt, DIMS>& P, unsigned& n, int cmin, Writ
 // drops sit at fixed trips.
 // (STOP: the lowest plane coded, STOP even; planes STOP-1 .. 0 are left to a
 // later call, as the 2D split of encode_block does)
-template <int H, int C, bool PRI = true, int STOP = 0, typename UInt, int DIMS, bool VEC, typename Writer>
-ZFP_HD bool encode_half_fixed(const planes<UInt, DIMS, VEC>& P, unsigned& n, Writer& wr) {
+template <int H, int C, bool PRI = true, int STOP = 0, typename UInt, int DIMS, typename Writer>
+ZFP_HD bool encode_half_fixed(const planes<UInt, DIMS>& P, unsigned& n, Writer& wr) {
   typedef typename plane_word<DIMS>::type PW;
   if constexpr (C >= STOP + 1) {
     if (!any_lane(!wr.full())) return false;
@@ -1884,14 +1860,20 @@ ZFP_HD PW decode_plane_any(unsigned& n, Reader& rd) {
 // position N-1 (one wave-uniform test covers both).
 
 
-template <int DIMS, typename PW, typename Reader>
+// PIN / POUT (pipelined readers): this step's windows were issued by the
+// previous step / this step issues the next step's
+template <int DIMS, typename PW, bool PIN = false, bool POUT = false, typename Reader>
 ZFP_HD PW decode_plane_fast_any(unsigned& n, Reader& rd) {
   constexpr unsigned N = 1u << (2 * DIMS);
   const unsigned nf = n;  // <= N-1
   // the group window first (the lookups wait on it), the verbatim window's
   // reads after the lookups' (Reader::window_g / window_w)
   WRaw wr;
-  const uint32_t g = rd.window_g(nf, wr);
+  uint32_t g;
+  if constexpr (pipe_of<Reader>::value && PIN)
+    g = rd.window_g_pipe(wr);  // issued by the previous step (or the loop's prologue)
+  else
+    g = rd.window_g(nf, wr);
   uint32_t e1, e2, sel = 0, e2a = 0, e2b = 0;
   if constexpr (DIMS == 1)
     e1 = rd.chunk1_fast(g);  // a 1D code fits chunk 1
@@ -1918,6 +1900,14 @@ ZFP_HD PW decode_plane_fast_any(unsigned& n, Reader& rd) {
   // (the biased count laundered: the compiler otherwise distributes the shift,
   // (nfp << 25) + (64 - N) << 25, and re-materialises that constant every step)
   const int32_t rare = (int32_t)(S | ((N == 64 ? nfp : launder(nfp + (64u - N))) << 25));
+  // pipelined readers: the next step's windows are read now, at the common
+  // path's next position (the clip below) and n (nfp < N there; & 63 bounds
+  // the rare path's, whose reads are re-issued after it)
+  uint32_t np = 0;
+  if constexpr (pipe_of<Reader>::value && POUT) {
+    np = umin(rd.pos + nf + ent_used(S), rd.end);
+    rd.prefetch_at(np, nfp & 63u);
+  }
   if (__builtin_expect(any_lane(rare < 0), 0)) {
     const auto pos0 = rd.pos;
     // The budget-aware resolution from the entries already read
@@ -1944,6 +1934,7 @@ ZFP_HD PW decode_plane_fast_any(unsigned& n, Reader& rd) {
     // leave no LDS read of the rare paths in flight: the common path's wait
     // bookkeeping after the join then needs no extra waits of its own
     rd.lds_wait();
+    if constexpr (pipe_of<Reader>::value && POUT) rd.prefetch_at(rd.pos, n);
     return x;
   }
   ZFP_COUNT_PATH(0);
@@ -1968,7 +1959,10 @@ ZFP_HD PW decode_plane_fast_any(unsigned& n, Reader& rd) {
     x = merge_at<PW>(nf, ones, w);
   }
   n = nfp;
-  rd.pos = umin(rd.pos + nf + ent_used(S), rd.end);
+  if constexpr (pipe_of<Reader>::value && POUT)
+    rd.pos = np;
+  else
+    rd.pos = umin(rd.pos + nf + ent_used(S), rd.end);
   return x;
 }
 
@@ -1979,13 +1973,14 @@ template <int H, typename UInt, int DIMS, typename Reader>
 ZFP_HD int decode_half(planes<UInt, DIMS>& P, unsigned& n, int cmin, Reader& rd) {
   typedef typename plane_word<DIMS>::type PW;
   int c = 31;
+  if constexpr (pipe_of<Reader>::value && kPipeAll) rd.prefetch_at(rd.pos, n);  // the first step's windows
   for (; c - 1 >= cmin; c -= 2) {
     if (!any_lane(rd.pos < rd.end)) return c;
     if constexpr (prio_of<Reader>::value)
       progress_priority<CUZFP_DPRIO_T2, CUZFP_DPRIO_T1, CUZFP_DPRIO_T0>(uniform(c));
     PW xa, xb;
-    xa = decode_plane_fast_any<DIMS, PW>(n, rd);
-    xb = decode_plane_fast_any<DIMS, PW>(n, rd);
+    xa = decode_plane_fast_any<DIMS, PW, kPipeAll, true>(n, rd);
+    xb = decode_plane_fast_any<DIMS, PW, true, kPipeAll>(n, rd);
     ZFP_STAMP(4);  // diagnostic builds: the last fast pair's end
     const int u = uniform(c);
     P.template set<H>(u, xa);
@@ -2009,13 +2004,12 @@ ZFP_HD int decode_half(planes<UInt, DIMS>& P, unsigned& n, int cmin, Reader& rd)
 // into the layout its indexed moves use).  1D/2D planes share registers and
 // set() ORs, so that array is zeroed up front.  (CUZFP_EAGER_ZERO: zero up
 // front in 3D too.)
-// 3D 64-bit blocks: the low half's planes transposed in two parts, bit 0 the
-// encoder (planes::load_split), bit 1 the decoder (planes::store_split)
+// 3D 64-bit encoder: the low half's planes transposed in two parts
+// (planes::load_split; 0: the whole block up front).  (The decoder's mirror
+// image -- the inverse transpose from rows 16..31 when planes 15..0 are unset
+// on every lane -- measured no gain, r06_ab_f64split.txt, and is not built.)
 #ifndef CUZFP_F64_SPLIT
-#define CUZFP_F64_SPLIT 0
-#endif
-#ifndef CUZFP_F64_SPLIT_VEC
-#define CUZFP_F64_SPLIT_VEC true
+#define CUZFP_F64_SPLIT 1
 #endif
 #ifndef CUZFP_EAGER_ZERO
 constexpr bool kLazyZero = true;
@@ -2048,8 +2042,8 @@ ZFP_HD int decode_half_fixed(planes<UInt, DIMS>& P, unsigned& n, Reader& rd) {
       else if constexpr (C == CUZFP_DPRIO_T0) __builtin_amdgcn_s_setprio(0);
     }
 #endif
-    const PW xa = decode_plane_fast_any<DIMS, PW>(n, rd);
-    const PW xb = decode_plane_fast_any<DIMS, PW>(n, rd);
+    const PW xa = decode_plane_fast_any<DIMS, PW, kPipeAll, true>(n, rd);
+    const PW xb = decode_plane_fast_any<DIMS, PW, true, kPipeAll>(n, rd);
     ZFP_STAMP(4);  // diagnostic builds: the last pair's end
     P.template set<H>(C, xa);
     P.template set<H>(C - 1, xb);
@@ -2093,9 +2087,8 @@ ZFP_HD void decode_planes_1d(planes<UInt, 1>& P, uint32_t& n12, Reader& rd) {
   }
 }
 
-// Returns the highest plane left unset by a 32-bit coefficients' loop, or by
-// the low half's loop of 64-bit ones (-1: none; every plane below it is unset
-// too), 31 where nothing is known.
+// Returns the highest plane left unset by a 32-bit coefficients' loop (-1:
+// none; every plane below it is unset too), 31 otherwise (nothing known).
 template <typename UInt, int DIMS, typename Reader>
 ZFP_HD int decode_planes(planes<UInt, DIMS>& P, unsigned budget, unsigned maxprec, Reader& rd) {
   constexpr int PREC = (int)sizeof(UInt) * 8;
@@ -2111,6 +2104,7 @@ ZFP_HD int decode_planes(planes<UInt, DIMS>& P, unsigned budget, unsigned maxpre
       decode_planes_1d<0, 31>(P, n12, rd);
       return 31;
     }
+    if constexpr (pipe_of<Reader>::value && kPipeAll) rd.prefetch_at(rd.pos, 0);  // the first step's windows
     return decode_half_fixed<0, 31>(P, n, rd);
   } else {
     const int kmin = PREC > (int)maxprec ? PREC - (int)maxprec : 0;
@@ -2129,10 +2123,7 @@ ZFP_HD int decode_planes(planes<UInt, DIMS>& P, unsigned budget, unsigned maxpre
       zero_planes<0>(P, 31);
       return 31;
     }
-    // the low half's highest unset plane (3D: planes::store_split)
-    const int c = decode_half<0>(P, n, kmin, rd);
-    zero_planes<0>(P, c);
-    return c;
+    zero_planes<0>(P, decode_half<0>(P, n, kmin, rd));
   }
   return 31;
 }
@@ -2387,12 +2378,13 @@ ZFP_HD void encode_block(const Scalar* f, unsigned maxbits, Writer& wr) {
       P.template load<true>(u);
       encode_half_fixed<0, 15>(P, n, wr);
     }
-  } else if constexpr ((CUZFP_F64_SPLIT & 1) && DIMS == 3 && sizeof(UInt) == 8) {
+  } else if constexpr (CUZFP_F64_SPLIT && DIMS == 3 && sizeof(UInt) == 8 && zero_inline_of<Writer>::value) {
     // 3D 64-bit blocks: the low half's tiles transposed a 16-plane part at a
     // time, each only if some lane of the wave still has budget
-    // (planes::load_split).  One consumer of u, in plain registers: a second
-    // layout of u for the rolled loops' tuples made the kernel spill.
-    planes<UInt, DIMS, CUZFP_F64_SPLIT_VEC> PS;
+    // (planes::load_split), in the lane-interleaved image's kernels (with the
+    // bit-packed image the kernel spills in its main path).  One consumer of u: a second layout of u for a
+    // separate rolled path made the kernel spill in its main path.
+    planes<UInt, DIMS> PS;
     PS.template load_split<true>(u);
     ZFP_STAMP(3);
     unsigned n = 0;
@@ -2405,22 +2397,10 @@ ZFP_HD void encode_block(const Scalar* f, unsigned maxbits, Writer& wr) {
         }
       }
     } else {  // some lane stops above plane 0: encode_planes' rolled loops
-#ifndef CUZFP_TMP_NOELSE
       PS.template lo_part<true, true>();
       PS.template lo_part<true, false>();
       const int kmin = 64 - (int)maxprec;
-      if constexpr (CUZFP_F64_SPLIT_VEC) {
-        if (encode_half<1>(PS, n, kmin > 32 ? kmin - 32 : 0, wr)) encode_half<0>(PS, n, kmin, wr);
-      } else {
-#pragma unroll
-        for (int h = 0; h < 2; h++)
-#pragma unroll
-          for (int g = 0; g < 2; g++)
-#pragma unroll
-            for (int r = 0; r < 32; r++) P.w.set(h, g, r, PS.w.get(h, g, r));
-        if (encode_half<1>(P, n, kmin > 32 ? kmin - 32 : 0, wr)) encode_half<0>(P, n, kmin, wr);
-      }
-#endif
+      if (encode_half<1>(PS, n, kmin > 32 ? kmin - 32 : 0, wr)) encode_half<0>(PS, n, kmin, wr);
     }
   } else {
     P.template load<true>(u);
@@ -2505,15 +2485,6 @@ ZFP_HD bool decode_block(Scalar* f, unsigned maxbits, Reader& rd) {
       permute_inv_sub<DIMS>(u, q, NB, make_seq<N>());  // (u ^ NB) - NB
     }
     ZFP_STAMP(2);
-  } else if constexpr ((CUZFP_F64_SPLIT & 2) && DIMS == 3 && sizeof(UInt) == 8) {
-    // planes 15..0 unset on every lane of the wave (BASELINE's 3D f64 rate 16
-    // stops above plane 20): the low half's tiles from rows 16..31 alone
-    if (unset >= 15)
-      P.template store_split<true>(u);  // u ^ NB
-    else
-      P.template store<true>(u);
-    ZFP_STAMP(2);
-    permute_inv_sub<DIMS>(u, q, NB, make_seq<N>());  // (u ^ NB) - NB
   } else {
     P.template store<true>(u);  // u ^ NB
     ZFP_STAMP(2);
