@@ -332,31 +332,6 @@ struct LdsReader {
   __device__ __forceinline__ uint64_t window_w_make(const WRaw& a) const {
     return (uint64_t)__builtin_amdgcn_alignbit(a.a1, a.a0, pos) | ((uint64_t)__builtin_amdgcn_alignbit(a.a2, a.a1, pos) << 32);
   }
-  // Pipelined windows (CUZFP_DPIPE): a fast step issues the next step's reads
-  // -- the group window at p + m, the 64-bit window at p -- as soon as it
-  // knows the next position, before its own rare-path test and merge, and the
-  // next step starts from them (window_g_pipe).  Every LDS read of a step's
-  // chain then leaves ~a dozen instructions earlier.
-  static constexpr bool kPipe = CUZFP_DPIPE != 0;
-  uint32_t pq, pb0, pb1;
-  WRaw pwr;
-  __device__ __forceinline__ void prefetch_at(uint32_t p, uint32_t m) {
-    pq = p + m;
-    lds_u32* t = row(pq);
-    pb0 = t[0];
-    pb1 = t[64];
-    __builtin_amdgcn_sched_barrier(0);
-    lds_u32* r = row(p);
-    pwr = WRaw{r[0], r[64], r[128]};
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  __device__ __forceinline__ uint32_t window_g_pipe(WRaw& wr) const {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_waitcnt(0xc27f);  // lgkmcnt(2): the group window (issued first)
-    __builtin_amdgcn_sched_barrier(0);
-    wr = pwr;
-    return __builtin_amdgcn_alignbit(pb1, pb0, pq);
-  }
   // every LDS read issued so far has landed (s_waitcnt lgkmcnt(0))
   __device__ __forceinline__ void lds_wait() const { __builtin_amdgcn_s_waitcnt(0xc07f); }
   // The chunk tables are the kernel's static LDS (address 0), so an entry's
@@ -470,7 +445,6 @@ struct LdsReader {
 // chunk 1's 8-byte entries (one AND instead of a shift and an AND).
 template <bool PRIO = true, bool B32 = false>
 struct RegReader : LdsReader<PRIO> {
-  static constexpr bool kPipe = false;  // its windows are register shifts
   uint64_t blk, blk8;
   __device__ __forceinline__ void set_block(uint64_t b) {
     blk = b;

@@ -797,20 +797,6 @@ ZFP_HD bool any_lane(bool p) {
 #define CUZFP_DPRIO_T0 (-1)
 #define CUZFP_DPRIO_AFTER 2
 #endif
-// the LDS reader's pipelined windows (LdsReader::prefetch_at): 1 every fast
-// step issues the next one's reads, 2 the first step of each pair only
-#ifndef CUZFP_DPIPE
-#define CUZFP_DPIPE 0
-#endif
-constexpr bool kPipeAll = CUZFP_DPIPE == 1;
-// Readers with pipelined windows: prefetch_at(p, m) issues the reads of the
-// windows at p + m and p, window_g_pipe(wr) takes them (kPipe)
-template <typename T, typename = void> struct pipe_of {
-  static constexpr bool value = false;
-};
-template <typename T> struct pipe_of<T, decltype((void)T::kPipe)> {
-  static constexpr bool value = T::kPipe;
-};
 // The schedule pays off when the launch is one resident round of waves (256^3
 // f32: 4 waves per SIMD, all resident at once).  Over several rounds it costs
 // 12 % (1024^3: step 3.63 -> 3.19 ms without it; tools/variants.py): a wave
@@ -1860,20 +1846,14 @@ ZFP_HD PW decode_plane_any(unsigned& n, Reader& rd) {
 // position N-1 (one wave-uniform test covers both).
 
 
-// PIN / POUT (pipelined readers): this step's windows were issued by the
-// previous step / this step issues the next step's
-template <int DIMS, typename PW, bool PIN = false, bool POUT = false, typename Reader>
+template <int DIMS, typename PW, typename Reader>
 ZFP_HD PW decode_plane_fast_any(unsigned& n, Reader& rd) {
   constexpr unsigned N = 1u << (2 * DIMS);
   const unsigned nf = n;  // <= N-1
   // the group window first (the lookups wait on it), the verbatim window's
   // reads after the lookups' (Reader::window_g / window_w)
   WRaw wr;
-  uint32_t g;
-  if constexpr (pipe_of<Reader>::value && PIN)
-    g = rd.window_g_pipe(wr);  // issued by the previous step (or the loop's prologue)
-  else
-    g = rd.window_g(nf, wr);
+  const uint32_t g = rd.window_g(nf, wr);
   uint32_t e1, e2, sel = 0, e2a = 0, e2b = 0;
   if constexpr (DIMS == 1)
     e1 = rd.chunk1_fast(g);  // a 1D code fits chunk 1
@@ -1900,14 +1880,6 @@ ZFP_HD PW decode_plane_fast_any(unsigned& n, Reader& rd) {
   // (the biased count laundered: the compiler otherwise distributes the shift,
   // (nfp << 25) + (64 - N) << 25, and re-materialises that constant every step)
   const int32_t rare = (int32_t)(S | ((N == 64 ? nfp : launder(nfp + (64u - N))) << 25));
-  // pipelined readers: the next step's windows are read now, at the common
-  // path's next position (the clip below) and n (nfp < N there; & 63 bounds
-  // the rare path's, whose reads are re-issued after it)
-  uint32_t np = 0;
-  if constexpr (pipe_of<Reader>::value && POUT) {
-    np = umin(rd.pos + nf + ent_used(S), rd.end);
-    rd.prefetch_at(np, nfp & 63u);
-  }
   if (__builtin_expect(any_lane(rare < 0), 0)) {
     const auto pos0 = rd.pos;
     // The budget-aware resolution from the entries already read
@@ -1934,7 +1906,6 @@ ZFP_HD PW decode_plane_fast_any(unsigned& n, Reader& rd) {
     // leave no LDS read of the rare paths in flight: the common path's wait
     // bookkeeping after the join then needs no extra waits of its own
     rd.lds_wait();
-    if constexpr (pipe_of<Reader>::value && POUT) rd.prefetch_at(rd.pos, n);
     return x;
   }
   ZFP_COUNT_PATH(0);
@@ -1959,10 +1930,7 @@ ZFP_HD PW decode_plane_fast_any(unsigned& n, Reader& rd) {
     x = merge_at<PW>(nf, ones, w);
   }
   n = nfp;
-  if constexpr (pipe_of<Reader>::value && POUT)
-    rd.pos = np;
-  else
-    rd.pos = umin(rd.pos + nf + ent_used(S), rd.end);
+  rd.pos = umin(rd.pos + nf + ent_used(S), rd.end);
   return x;
 }
 
@@ -1973,14 +1941,13 @@ template <int H, typename UInt, int DIMS, typename Reader>
 ZFP_HD int decode_half(planes<UInt, DIMS>& P, unsigned& n, int cmin, Reader& rd) {
   typedef typename plane_word<DIMS>::type PW;
   int c = 31;
-  if constexpr (pipe_of<Reader>::value && kPipeAll) rd.prefetch_at(rd.pos, n);  // the first step's windows
   for (; c - 1 >= cmin; c -= 2) {
     if (!any_lane(rd.pos < rd.end)) return c;
     if constexpr (prio_of<Reader>::value)
       progress_priority<CUZFP_DPRIO_T2, CUZFP_DPRIO_T1, CUZFP_DPRIO_T0>(uniform(c));
     PW xa, xb;
-    xa = decode_plane_fast_any<DIMS, PW, kPipeAll, true>(n, rd);
-    xb = decode_plane_fast_any<DIMS, PW, true, kPipeAll>(n, rd);
+    xa = decode_plane_fast_any<DIMS, PW>(n, rd);
+    xb = decode_plane_fast_any<DIMS, PW>(n, rd);
     ZFP_STAMP(4);  // diagnostic builds: the last fast pair's end
     const int u = uniform(c);
     P.template set<H>(u, xa);
@@ -2042,8 +2009,8 @@ ZFP_HD int decode_half_fixed(planes<UInt, DIMS>& P, unsigned& n, Reader& rd) {
       else if constexpr (C == CUZFP_DPRIO_T0) __builtin_amdgcn_s_setprio(0);
     }
 #endif
-    const PW xa = decode_plane_fast_any<DIMS, PW, kPipeAll, true>(n, rd);
-    const PW xb = decode_plane_fast_any<DIMS, PW, true, kPipeAll>(n, rd);
+    const PW xa = decode_plane_fast_any<DIMS, PW>(n, rd);
+    const PW xb = decode_plane_fast_any<DIMS, PW>(n, rd);
     ZFP_STAMP(4);  // diagnostic builds: the last pair's end
     P.template set<H>(C, xa);
     P.template set<H>(C - 1, xb);
@@ -2104,7 +2071,6 @@ ZFP_HD int decode_planes(planes<UInt, DIMS>& P, unsigned budget, unsigned maxpre
       decode_planes_1d<0, 31>(P, n12, rd);
       return 31;
     }
-    if constexpr (pipe_of<Reader>::value && kPipeAll) rd.prefetch_at(rd.pos, 0);  // the first step's windows
     return decode_half_fixed<0, 31>(P, n, rd);
   } else {
     const int kmin = PREC > (int)maxprec ? PREC - (int)maxprec : 0;
