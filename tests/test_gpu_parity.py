@@ -675,3 +675,28 @@ def test_golden_1024_slab(cuda, world, rank):
     torch.cuda.synchronize()
     assert words.numel() == sh.words
     assert hashlib.sha256(words.cpu().numpy().tobytes()).hexdigest() == gold[f"slab_sha256_n{world}"][rank]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [np.float64, np.int64])
+def test_split_transpose_64bit(cuda, restatement, dtype):
+    """The 3D 64-bit encoder's low-half planes, transposed 16 at a time only
+    while some lane of the wave has budget (zfp_block.hpp, planes::load_split):
+    rates that stop waves above plane 32, between 32 and 16 and below 16, in
+    aligned (lane-interleaved image) arrays, with waves mixing blocks of every
+    magnitude and, for doubles, tiny-exponent blocks (maxprec < 64: the rolled
+    path after the split transpose) beside normal ones."""
+    rng = np.random.default_rng(641)
+    shape = (8, 16, 256)  # whole waves of 64 blocks along x
+    if dtype == np.float64:
+        a = np.cumsum(rng.standard_normal(shape), axis=-1) * 10.0 ** rng.integers(-8, 8, size=shape)
+        a[:4, :4, :128] *= 1e-310  # tiny-exponent blocks in some waves
+    else:
+        a = (np.cumsum(rng.integers(-1 << 40, 1 << 40, size=shape), axis=-1) >> rng.integers(0, 40, size=shape))
+    a = a.astype(dtype)
+    for rate in (2, 6, 12, 20, 28, 36, 48, 64):
+        mb = cz.rate_to_maxbits(rate, dtype, 3)
+        words, y = _gpu_roundtrip(a, mb, cuda)
+        ref = restatement.compress(a, mb)
+        assert np.array_equal(words, ref), rate
+        assert np.array_equal(y.view(np.uint8), restatement.decompress(ref, a.shape, dtype, mb).view(np.uint8)), rate
