@@ -823,8 +823,16 @@ __device__ __forceinline__ void scatter_f64_staged(double* __restrict__ data, co
 #ifndef CUZFP_F64_DEC_WAVES  // A/B builds
 #define CUZFP_F64_DEC_WAVES 2
 #endif
+#ifndef CUZFP_F32_DEC_WAVES  // A/B builds: 3D float decoder / encoder
+#define CUZFP_F32_DEC_WAVES 4
+#endif
+#ifndef CUZFP_F32_ENC_WAVES
+#define CUZFP_F32_ENC_WAVES 4
+#endif
 template <typename Scalar, int DIMS, bool ENC = false> struct occupancy {
-  static constexpr int value = (sizeof(Scalar) == 8 && DIMS == 3) ? (ENC ? CUZFP_F64_ENC_WAVES : CUZFP_F64_DEC_WAVES) : 4;
+  static constexpr int value = (sizeof(Scalar) == 8 && DIMS == 3) ? (ENC ? CUZFP_F64_ENC_WAVES : CUZFP_F64_DEC_WAVES)
+                               : (sizeof(Scalar) == 4 && DIMS == 3) ? (ENC ? CUZFP_F32_ENC_WAVES : CUZFP_F32_DEC_WAVES)
+                                                                    : 4;
 };
 
 // REG (1D/2D, maxbits 32 or 64): the block is coded into a register
