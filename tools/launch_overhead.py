@@ -28,7 +28,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--reps", type=int, default=15)
+    ap.add_argument("--sched", choices=["auto", "spin", "yield", "blocking"], default="auto",
+                    help="hipSetDeviceFlags scheduling mode, set before the device is used")
     a = ap.parse_args()
+    if a.sched != "auto":
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so")
+        rc = hip.hipSetDeviceFlags({"spin": 1, "yield": 2, "blocking": 4}[a.sched])
+        print(f"hipSetDeviceFlags({a.sched}) -> {rc}", flush=True)
     import numpy as np
     import torch
     import cuzfp_amd as cz
@@ -78,10 +85,12 @@ def main():
             torch.cuda.synchronize()
             walls.append((time.perf_counter() - t0) / K * 1e6)
             gpus.append(e0.elapsed_time(e1) / K * 1e3)
+        walls_raw = list(walls)
         walls.sort()
         gpus.sort()
+        first = walls_raw[0]
         out[name] = {"wall_us_per_step": round(walls[len(walls) // 2], 2), "gpu_us_per_step": round(gpus[len(gpus) // 2], 2),
-                     "wall_min": round(walls[0], 2)}
+                     "wall_min": round(walls[0], 2), "wall_max": round(walls[-1], 2), "wall_first": round(first, 2)}
         print(name, out[name], flush=True)
     print(json.dumps(out))
 
