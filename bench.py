@@ -539,6 +539,22 @@ def finish_other_configs(st: list) -> list:
                              "max_abs_err_matches_reference": (err == g["max_abs_err"]) if g else None,
                              "golden_case": s["key"]}
             rec["parity_ok"] = bool(g) and got == g["stream_sha256"] and dec == g["decoded_sha256"]
+        # roofline.traffic: the dominant kernel's HBM bytes a launch from the
+        # builder's PMC session for this workload (profiles/traffic_configs.json)
+        tpath = os.path.join(ROOT, "profiles", "traffic_configs.json")
+        roof = rec.get("roofline")
+        if roof is not None and os.path.exists(tpath):
+            try:
+                tj = json.load(open(tpath)).get(rec.get("workload"))
+            except (OSError, ValueError):
+                tj = None
+            kind = "decode" if roof.get("kernel") == "zfp_decode" else "encode"
+            if tj and tj.get(kind + "_hbm_bytes_per_launch"):
+                roof["traffic"] = tj[kind + "_hbm_bytes_per_launch"]
+                roof["traffic_source"] = {"file": "profiles/traffic_configs.json", "session": tj.get("source"),
+                                          "method": tj.get("method"),
+                                          "note": "PMC counters of an earlier profiled session of this workload, "
+                                                  "not of this run"}
         recs.append(rec)
         s.clear()
     torch.cuda.empty_cache()

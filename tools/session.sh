@@ -94,6 +94,17 @@ for s in "$@"; do
       timeout -s KILL 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_${TAG}/write" -o run -- \
         python tools/kernel_probe.py > /dev/null 2>&1
       stop_on $? pmc_write ;;
+    pmccfg)  # PMC traffic of BASELINE configs[2] (3D f64 256^3 r16) and configs[3] (2D f32 8192^2 r2)
+      for cfg in "f64:--dtype float64 --rate 16" "2d:--dims 2 --size 8192 --rate 2"; do
+        name=${cfg%%:*}; args=${cfg#*:}
+        rm -rf "$OUT/pmc_${name}_${TAG}"
+        timeout -s KILL 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_${name}_${TAG}/fetch" -o run -- \
+          python tools/kernel_probe.py $args > /dev/null 2>&1
+        stop_on $? pmccfg_${name}_fetch
+        timeout -s KILL 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_${name}_${TAG}/write" -o run -- \
+          python tools/kernel_probe.py $args > /dev/null 2>&1
+        stop_on $? pmccfg_${name}_write
+      done ;;
     counters)
       i=0
       for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_INSTS_VMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY" \
