@@ -132,7 +132,7 @@ def table(ks):
 
 
 def counters(path: str) -> dict:
-    """SQ_INSTS_VALU / SQ_WAVES of the 3D f32 kernels in a tools/counters.py report"""
+    """SQ_INSTS_* / SQ_WAVES of the 3D f32 kernels in a tools/counters.py report"""
     out, kind, vals = {}, None, {}
     for line in open(path):
         m = re.match(r"^zfp_(encode|decode)<float, 3, true, true", line)
@@ -142,8 +142,9 @@ def counters(path: str) -> dict:
         m = re.match(r"^\s+(SQ_\w+)\s+([0-9.e+]+)", line)
         if kind and m:
             vals[m.group(1)] = float(m.group(2))
-            if "SQ_INSTS_VALU" in vals and "SQ_WAVES" in vals:
-                out[kind] = vals["SQ_INSTS_VALU"] / vals["SQ_WAVES"]
+            if "SQ_WAVES" in vals:
+                out[kind] = {k[len("SQ_INSTS_"):]: v / vals["SQ_WAVES"] for k, v in vals.items()
+                             if k.startswith("SQ_INSTS_")}
     return out
 
 
@@ -174,14 +175,16 @@ def main():
         extra = (DEC_RARE if kind == "decode" else ENC_WIDE)
         print(f"{'(not priced: ' + ('rare-path steps' if kind == 'decode' else 'wide steps') + f', ~{extra} a wave)':66s}")
         print(f"{'total, priced':66s} {tot[0]:7.0f} {tot[1]:7.0f} {tot[2]:7.0f} {tot[3]:9.0f} {tot[4]:9.1f}")
-        if kind in dyn:
-            v = dyn[kind]
-            print(f"{'dynamic (SQ counters): VALU a wave, SQ_INSTS_VALU / SQ_WAVES':66s} {v:7.0f}")
+        if kind in dyn and "VALU" in dyn[kind]:
+            d = dyn[kind]
+            print(f"{'dynamic (SQ counters): VALU a wave, SQ_INSTS_VALU / SQ_WAVES':66s} {d['VALU']:7.0f}")
+            other = ", ".join(f"{k} {d[k]:.0f}" for k in ("SALU", "LDS", "BRANCH", "VMEM", "SMEM") if k in d)
+            print(f"{'  beside them a wave issues (not priced): ' + other}")
         us = a.enc_us if kind == "encode" else a.dec_us
         if us:
             wall = us * 1e-6 * CLOCK_GHZ * 1e9 / BLOCKS_PER_SIMD
             print(f"{'measured kernel time ' + f'{us:.1f} us':66s} {'':7s} {'':7s} {'':7s} {'':9s} {wall:9.1f}")
-            print(f"{'  issue share of the wall time':66s} {'':31s} {100 * tot[4] / wall:8.0f}%")
+            print(f"{'  VALU-priced share of the wall time':66s} {'':31s} {100 * tot[4] / wall:8.0f}%")
             print(f"{'  to reach 70 % of HBM: cut (cycles a block)':66s} {'':31s} {wall - budget:9.1f}")
         print()
 
