@@ -373,14 +373,10 @@ struct LdsReader {
   // then runs past position N-1, which the steps' implied-one rule resolves.)
   __device__ __forceinline__ void chunks_fast(uint32_t g, uint32_t& e1, uint32_t& sel, uint32_t& e2a,
                                               uint32_t& e2b) const {
-#if defined(CUZFP_DMASK)  // A/B: lanes whose leading group test is "0" read entry 0 (a broadcast)
-    const uint32_t m = (uint32_t)((int32_t)(g << 31) >> 31);
-    const uint2 c = tab64(off1(g) & m);
-    const uint2 p = tab64(kPairBytes + (CUZFP_DMASK == 2 ? off2(g) & m : off2(g)));
-#else
+    // (sending the lookups of lanes whose leading test is "0" to entry 0, a
+    // broadcast, measured neutral in round 6: profiles/r06_ab_dmask.txt)
     const uint2 c = tab64(off1(g));
     const uint2 p = tab64(kPairBytes + off2(g));
-#endif
     e1 = c.x;
     sel = c.y;
     e2a = p.x;
