@@ -67,13 +67,19 @@ arr = polynomial_field(shape, {dtype!r}) if {field!r} == 'polynomial' else split
 x = torch.from_numpy(arr).cuda()
 mb = cz.rate_to_maxbits({rate}, arr.dtype, {dims})
 w = cz.encode(x, mb); y = cz.decode(w, shape, x.dtype, mb)
-def t(fn):
-    for _ in range(3): fn()
+def t(fn):  # a hipGraph of {reps} launches, median of 11 replays (eager launches can be host-bound)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range({reps}): fn()
+    g.replay(); torch.cuda.synchronize()
     e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize(); e0.record()
-    for _ in range({reps}): fn()
-    e1.record(); torch.cuda.synchronize()
-    return e0.elapsed_time(e1) / {reps} * 1000
+    r = []
+    for _ in range(11):
+        torch.cuda.synchronize(); e0.record()
+        g.replay()
+        e1.record(); torch.cuda.synchronize()
+        r.append(e0.elapsed_time(e1) / {reps} * 1000)
+    return sorted(r)[5]
 print(json.dumps(dict(enc_us=t(lambda: cz.encode(x, mb, out=w)), dec_us=t(lambda: cz.decode(w, shape, x.dtype, mb, out=y)))))
 """
         r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
